@@ -1,0 +1,267 @@
+#!/usr/bin/env python3
+"""Generate golden vectors by running the REFERENCE implementation.
+
+Run in the build container only (needs /root/reference, read-only):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+It imports the reference package ``dlsa`` from /root/reference through a
+minimal compatibility shim (the reference targets numpy<1.24, pandas<2 and
+sklearn<1.2; SURVEY.md 8(c) "Oracle recipe"):
+
+* ``dlsa.models.LogisticRegression``  -> factory mapping ``penalty='none'``
+  to ``None`` and forcing ``tol`` (1e-12 for parity; 1e-4 = sklearn default
+  also recorded);
+* ``dlsa.models.pd``                  -> proxy whose ``concat(objs, 1)``
+  forwards ``axis=1``;
+* ``np.float = float; np.NAN = np.nan`` before ``import dlsa.lsa``.
+
+Nothing of the reference is copied: only inputs and the reference's outputs
+are written, as ``tests/golden/*.npz``.  Large inputs are not stored; they are
+regenerated from the recorded seed by the vectorised generator, which this
+script first checks to be bit-identical with the reference's
+``simulate_logistic``.
+"""
+
+import os
+import sys
+import warnings
+
+sys.dont_write_bytecode = True
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REF)
+sys.path.insert(0, os.path.abspath(os.path.join(OUT, "..", "..")))
+
+import numpy as np  # noqa: E402
+import pandas as pd  # noqa: E402
+from sklearn.linear_model import LogisticRegression as _SkLR  # noqa: E402
+from sklearn.linear_model import lars_path_gram  # noqa: E402
+
+warnings.filterwarnings("ignore")
+
+import dlsa.models as RM  # noqa: E402  (reference)
+
+np.float = float  # shim for dlsa/lsa.py:12,90
+np.NAN = np.nan   # shim for dlsa/lsa.py:23
+import dlsa.lsa as RL  # noqa: E402  (reference)
+
+from oracle.dlsa_oracle import simulate_logistic_arrays  # noqa: E402
+
+_TOL = [1e-12]
+
+
+def _lr_factory(**kw):
+    if kw.get("penalty") == "none":
+        kw["penalty"] = None
+    kw["tol"] = _TOL[0]
+    return _SkLR(**kw)
+
+
+class _PdProxy:
+    def __getattr__(self, name):
+        return getattr(pd, name)
+
+    @staticmethod
+    def concat(objs, *args, **kw):
+        if args:
+            kw["axis"] = args[0]
+        return pd.concat(objs, **kw)
+
+
+RM.LogisticRegression = _lr_factory
+RM.pd = _PdProxy()
+
+
+def ref_map(df, y_name, fit_intercept, data_info=None, tol=1e-12):
+    """Reference map stage: logistic_model per partition group, in partition
+    order (projects/logistic_dlsa.py:325)."""
+    _TOL[0] = tol
+    outs = []
+    for _, g in df.groupby("partition_id", sort=True):
+        # Spark's GROUPED_MAP pandas_udf builds each group from Arrow with a
+        # fresh RangeIndex; models.py:119-120 relies on it.
+        g = g.reset_index(drop=True)
+        kw = {}
+        if data_info is not None:
+            kw["data_info"] = data_info
+        o = RM.logistic_model(g, y_name, fit_intercept=fit_intercept, **kw)
+        outs.append(o.to_numpy(dtype=np.float64))
+    return np.stack(outs)  # [K, p, p+3]: par_id, coef, Sig_invMcoef, Sig_inv
+
+
+def combine(outs, K):
+    """dlsa_mapred restated (Spark absent): group-sum + lstsq (dlsa.py:30-52)."""
+    S = outs[:, :, 3:].sum(0)
+    v = outs[:, :, 2].sum(0)
+    wlse = np.linalg.lstsq(S, v, rcond=None)[0]
+    oneshot = outs[:, :, 1].sum(0) / K
+    return wlse, oneshot, S
+
+
+def ref_lars(S, b, n, typ):
+    r = RL.lars_lsa(np.matrix(S), np.asarray(b, float), intercept=False, n=n,
+                    type=typ)
+    return (np.asarray(r["AIC"]).ravel(), np.asarray(r["BIC"]).ravel(),
+            np.asarray(r["beta"]), np.asarray(r["beta0"]).ravel())
+
+
+def sk_lars(S, b, typ):
+    """Independent oracle: sklearn lars_path_gram on the scaled problem."""
+    D = np.abs(b)
+    G = D[:, None] * S * D[None, :]
+    Xy = G @ np.sign(b)
+    _, _, coefs = lars_path_gram(Xy=Xy, Gram=G, n_samples=10 ** 6,
+                                 method=typ, eps=np.finfo(float).eps)
+    return (coefs * D[:, None]).T
+
+
+def main():
+    rng_report = {}
+
+    # ---- A. simulate_logistic bit-identity ---------------------------------
+    for (seed, n, p, K) in [(2019, 3000, 10, 4), (7, 600, 7, 3)]:
+        np.random.seed(seed)
+        ref_df = RM.simulate_logistic(n, p, "systematic", K)
+        np.random.seed(seed)
+        pid, lab, feat = simulate_logistic_arrays(n, p, "systematic", K)
+        mine = np.concatenate([pid[:, None], lab[:, None], feat], 1)
+        ref = ref_df.to_numpy(np.float64)
+        assert np.array_equal(ref, mine), "vectorised generator differs"
+        np.savez_compressed(os.path.join(OUT, f"simulate_s{seed}_n{n}_p{p}_K{K}.npz"),
+                            seed=seed, n=n, p=p, K=K, data=ref)
+        rng_report[(seed, n, p)] = "bit-identical"
+    print("simulate: bit-identical", rng_report)
+
+    # ---- B. config 1 (n=1e5, p=10, K=4, seed 2019) -------------------------
+    np.random.seed(2019)
+    pid, lab, feat = simulate_logistic_arrays(100000, 10, "systematic", 4)
+    cols = ["x" + str(i) for i in range(10)]
+    df = pd.DataFrame(np.concatenate([pid[:, None], lab[:, None], feat], 1),
+                      columns=["partition_id", "label"] + cols)
+    rec = dict(seed=2019, n=100000, p=10, K=4,
+               checksum_X=float(feat.sum()), checksum_y=float(lab.sum()))
+    for fi in (False, True):
+        outs = ref_map(df, "label", fi, tol=1e-12)
+        outs_def = ref_map(df, "label", fi, tol=1e-4)
+        wlse, oneshot, S = combine(outs, 4)
+        tag = "int" if fi else "noint"
+        rec[f"outs_{tag}"] = outs
+        rec[f"outs_deftol_{tag}"] = outs_def
+        rec[f"wlse_{tag}"] = wlse
+        rec[f"oneshot_{tag}"] = oneshot
+        if not fi:
+            for typ in ("lar", "lasso"):
+                AIC, BIC, beta, beta0 = ref_lars(S, wlse, 100000, typ)
+                rec[f"lars_{typ}_AIC"] = AIC
+                rec[f"lars_{typ}_BIC"] = BIC
+                rec[f"lars_{typ}_beta"] = beta
+                sk = sk_lars(S, wlse, typ)
+                m = min(sk.shape[0], beta.shape[0])
+                print(f"config1 lars {typ}: ref vs sklearn max|d|",
+                      np.abs(sk[:m] - beta[:m]).max())
+        else:
+            try:
+                RL.lars_lsa(np.matrix(S), wlse, intercept=True, n=100000)
+                rec["ref_intercept_lars_error"] = "none"
+            except Exception as e:  # lsa.py:100 indexes range(1, n)
+                rec["ref_intercept_lars_error"] = type(e).__name__
+                print("reference lars_lsa(intercept=True) raises", type(e).__name__)
+    np.savez_compressed(os.path.join(OUT, "config1_n1e5_p10_K4.npz"), **rec)
+    print("config1 done; WLSE(noint) =", rec["wlse_noint"])
+
+    # ---- C. p=100, K=4, n_k=2e4 (seed 7) ----------------------------------
+    np.random.seed(7)
+    pid, lab, feat = simulate_logistic_arrays(80000, 100, "systematic", 4)
+    cols = ["x" + str(i) for i in range(100)]
+    df = pd.DataFrame(np.concatenate([pid[:, None], lab[:, None], feat], 1),
+                      columns=["partition_id", "label"] + cols)
+    outs = ref_map(df, "label", False, tol=1e-12)
+    outs_def = ref_map(df, "label", False, tol=1e-4)
+    wlse, oneshot, S = combine(outs, 4)
+    AIC, BIC, beta, _ = ref_lars(S, wlse, 80000, "lasso")
+    np.savez_compressed(os.path.join(OUT, "p100_n8e4_K4.npz"), seed=7, n=80000,
+                        p=100, K=4, checksum_X=float(feat.sum()),
+                        checksum_y=float(lab.sum()), outs=outs,
+                        outs_deftol=outs_def, wlse=wlse, oneshot=oneshot,
+                        lars_lasso_AIC=AIC, lars_lasso_BIC=BIC,
+                        lars_lasso_beta=beta)
+    print("p100 done; default-tol rel err",
+          np.abs(outs_def[:, :, 1] - outs[:, :, 1]).max() /
+          np.abs(outs[:, :, 1]).max())
+
+    # ---- D. games-expand.csv (reference data file, no intercept) ----------
+    g = pd.read_csv(os.path.join(REF, "projects/results/data/games-expand.csv"))
+    Xg = g.drop(["label"], axis=1).to_numpy().astype(np.uint8)
+    yg = g["label"].to_numpy().astype(np.uint8)
+    gdf = g.copy().astype(np.float64)
+    gdf.insert(0, "partition_id", (np.arange(len(g)) % 2).astype(np.float64))
+    outs_g = ref_map(gdf, "label", False, tol=1e-12)
+    np.savez_compressed(os.path.join(OUT, "games_expand.npz"), X=Xg, y=yg,
+                        K=2, outs=outs_g)
+    print("games-expand done", outs_g[:, :, 1])
+
+    # ---- E. LARS cases with LASSO drop events -----------------------------
+    rs = np.random.RandomState(11)
+    cases = []
+    tries = 0
+    while len(cases) < 6 and tries < 5000:
+        tries += 1
+        m = int(rs.choice([6, 9, 14, 25]))
+        A = rs.randn(3 * m, m) @ np.diag(rs.uniform(0.3, 2.0, m))
+        A[:, 1] += 0.9 * A[:, 0]  # correlation makes drops likely
+        S = A.T @ A
+        b = rs.randn(m) * rs.uniform(0, 1, m) + (rs.rand(m) < 0.4) * 2
+        try:
+            lasso = ref_lars(S, b, 500, "lasso")
+            lar = ref_lars(S, b, 500, "lar")
+        except Exception:
+            continue
+        beta = lasso[2]
+        drop = bool(any(np.any((np.abs(beta[i - 1]) > 0) & (beta[i] == 0))
+                        for i in range(1, beta.shape[0])))
+        if drop or len(cases) < 2:
+            cases.append(dict(S=S, b=b, n=500, lasso=lasso, lar=lar,
+                              drop=drop))
+    rec = {}
+    for i, c in enumerate(cases):
+        rec[f"c{i}_S"] = c["S"]
+        rec[f"c{i}_b"] = c["b"]
+        rec[f"c{i}_drop"] = c["drop"]
+        for typ in ("lasso", "lar"):
+            AIC, BIC, beta, beta0 = c[typ]
+            rec[f"c{i}_{typ}_AIC"] = AIC
+            rec[f"c{i}_{typ}_BIC"] = BIC
+            rec[f"c{i}_{typ}_beta"] = beta
+            sk = sk_lars(c["S"], c["b"], typ)
+            mm = min(sk.shape[0], beta.shape[0])
+            print(f"lars case {i} {typ} drop={c['drop']}: ref vs sklearn",
+                  np.abs(sk[:mm] - beta[:mm]).max())
+    rec["ncases"] = len(cases)
+    np.savez_compressed(os.path.join(OUT, "lars_cases.npz"), **rec)
+
+    # ---- F. data_info-standardised case with intercept ---------------------
+    rs = np.random.RandomState(5)
+    n, p = 6000, 5
+    X = rs.randn(n, p) * np.array([1, 3, 0.5, 10, 2]) + np.array([0, 5, -1, 100, 3])
+    Xs = (X - X.mean(0)) / X.std(0, ddof=1)
+    yy = (rs.rand(n) < 1 / (1 + np.exp(-(0.5 + Xs @ np.array([1, -1, 0.5, 0, 0]))))).astype(float)
+    cols = ["a", "b", "c", "d", "e"]
+    df = pd.DataFrame(np.concatenate([(np.arange(n) % 3)[:, None], yy[:, None], X], 1),
+                      columns=["partition_id", "label"] + cols)
+    # Spark describe() layout: rows count, mean, stddev, min, max (strings)
+    info = pd.DataFrame({"summary": ["count", "mean", "stddev", "min", "max"]})
+    for j, c in enumerate(cols):
+        info[c] = [str(n), repr(float(X[:, j].mean())),
+                   repr(float(X[:, j].std(ddof=1))),
+                   repr(float(X[:, j].min())), repr(float(X[:, j].max()))]
+    outs = ref_map(df, "label", True, data_info=info, tol=1e-12)
+    np.savez_compressed(os.path.join(OUT, "standardized_intercept.npz"), X=X, y=yy,
+                        K=3, center=np.array([float(v) for v in info.iloc[1, 1:]]),
+                        scale=np.array([float(v) for v in info.iloc[2, 1:]]),
+                        outs=outs)
+    print("standardized done")
+
+
+if __name__ == "__main__":
+    main()
