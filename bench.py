@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""DLSA logistic fit benchmark (BASELINE.json metric, config 2).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One step = one complete DLSA fit of the GPU's shard: batched Newton/IRLS over
+all partitions (fp32-MFMA Hessian passes + the final fp64 pass whose Hessian
+is Sig_inv), local partition reduction in HBM, one RCCL all-reduce of the
+P^2+2P+1 sums across ranks, WLSE solve, LARS path and DBIC selection on the
+host.  Per GPU: n = 1e8 rows, p = 100, K = 1024 partitions (weak scaling:
+every rank owns its own 1e8 rows).  Data are synthetic, generated in HBM by
+the counter-based generator before the timed region.
+
+Rank 0 prints one JSON line (metric/value/... plus "roofline" for the dominant
+kernel and "cpu_baseline": the numpy oracle on a bounded sample on host cores).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "DLSA logistic fit rows/sec (node), n=1e8 p=100, 1/2/4/8 GPUs; HBM GB/s"
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
+FP64_MFMA_PEAK_TF = 78.6   # MI355X fp64 matrix (spec; = fp64 vector on CDNA4)
+FP32_MFMA_PEAK_TF = 157.3  # MI355X_MICROARCH.md: f32-input MFMA = vector rate
+
+
+def _cpu_worker(args):
+    """One partition of the CPU baseline: regenerate its rows from the counter
+    stream, fit with the numpy oracle (1 BLAS thread)."""
+    n, p, seed, row0 = args
+    from threadpoolctl import threadpool_limits
+
+    import oracle as O
+
+    with threadpool_limits(1):
+        X, y = O.simulate_counter(n, p, seed=seed, row0=row0)
+        t0 = time.perf_counter()
+        o = O.logistic_fit(X, y)
+        return time.perf_counter() - t0, int(o["iters"])
+
+
+def cpu_baseline(nk, p, n_parts, workers, seed=2019):
+    """Oracle (port) timed on host cores: n_parts partitions of nk rows, one
+    process per core, fit time only (data regeneration excluded)."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    jobs = [(nk, p, seed, k * nk) for k in range(n_parts)]
+    t0 = time.perf_counter()
+    with ctx.Pool(workers) as pool:
+        res = pool.map(_cpu_worker, jobs, chunksize=1)
+    wall = time.perf_counter() - t0
+    fit_s = sum(r[0] for r in res)
+    # throughput if all `workers` cores fit concurrently
+    rows_per_s = n_parts * nk / (fit_s / workers)
+    return {"value": rows_per_s, "unit": "rows/s", "cores": workers, "kind": "port",
+            "sample": f"{n_parts} partitions x {nk} rows x p={p} (config-2 partition shape), "
+                      f"numpy fp64 IRLS oracle, 1 BLAS thread per process, {workers} processes; "
+                      f"fit CPU time {fit_s:.1f} s, wall {wall:.1f} s incl. data regeneration",
+            "iters_mean": sum(r[1] for r in res) / len(res)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--n", type=int, default=100_000_000, help="rows per GPU")
+    ap.add_argument("--p", type=int, default=100)
+    ap.add_argument("--partitions", type=int, default=1024, help="partitions per GPU")
+    ap.add_argument("--hessian", default="mixed", choices=["mixed", "fp64"])
+    ap.add_argument("--tol", type=float, default=1e-10)
+    ap.add_argument("--cpu-parts", type=int, default=32)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--seed", type=int, default=2019)
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from dlsa_amd.dlsa import reduce_partitions_device, split_reduced
+    from dlsa_amd.lsa import lars_lsa
+    from dlsa_amd.models import logistic_model_batched, simulate_logistic_device
+
+    n, p, K = args.n, args.p, args.partitions
+    offsets = (np.arange(K + 1, dtype=np.int64) * n) // K
+    X, y = simulate_logistic_device(n, p, seed=args.seed, row0=rank * n, device=dev)
+    ws = torch.empty((1,), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+
+    n_global = n * world
+    stats_acc = []
+
+    def step(record):
+        nonlocal ws
+        fit = logistic_model_batched(X, y, offsets, hessian=args.hessian, tol=args.tol,
+                                     record_timing=record, workspace=ws, device=dev)
+        if ws.numel() < fit.stats["workspace_bytes"]:
+            ws = torch.empty((fit.stats["workspace_bytes"],), dtype=torch.uint8, device=dev)
+        buf = reduce_partitions_device(fit)
+        if world > 1:
+            dist.all_reduce(buf, op=dist.ReduceOp.SUM)  # RCCL over xGMI
+        S, v, st, Ksum = split_reduced(buf.cpu().numpy(), fit.P)
+        wlse = np.linalg.lstsq(S, v, rcond=None)[0]
+        lars = lars_lsa(S, wlse, False, n_global, type="lasso")
+        ib = int(np.argmin(lars["BIC"]))
+        support = np.nonzero(lars["beta"][ib])[0]
+        return fit, wlse, support
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        fit, wlse, support = step(True)
+        stats_acc.append(fit.stats)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    ms_per_step = elapsed / args.steps * 1e3
+    value = n_global * args.steps / elapsed
+
+    # ---- roofline of the dominant kernel (HIP events on the fit's stream) --
+    ms32 = sum(s["ms_pass_fp32"] for s in stats_acc)
+    ms64 = sum(s["ms_pass_fp64"] for s in stats_acc)
+    n32 = sum(s["passes_fp32"] for s in stats_acc)
+    n64 = sum(s["passes_fp64"] for s in stats_acc)
+    ms_solve = sum(s["ms_solve"] for s in stats_acc)
+    bytes_per_pass = n * (8 * p + 8)
+    NT = (p + 15) // 16
+    tiles = NT * (NT + 1) // 2
+    mfma_flops_per_pass = (n / 4.0) * tiles * (16 * 16 * 4 * 2)
+    alg_flops_per_pass = n * (p * (p + 1) + 4 * p + 20)
+    kern = {}
+    if n32:
+        avg = ms32 / n32
+        kern["irls_pass_fp32hess"] = {
+            "launches_per_step": n32 / args.steps, "avg_ms": avg,
+            "GBps": bytes_per_pass / (avg * 1e-3) / 1e9,
+            "mfma_TFps": mfma_flops_per_pass / (avg * 1e-3) / 1e12}
+    if n64:
+        avg = ms64 / n64
+        kern["irls_pass_fp64hess"] = {
+            "launches_per_step": n64 / args.steps, "avg_ms": avg,
+            "GBps": bytes_per_pass / (avg * 1e-3) / 1e9,
+            "mfma_TFps": mfma_flops_per_pass / (avg * 1e-3) / 1e12}
+    kern["newton_solve"] = {"launches_per_step": (n32 + n64) / args.steps / max(1, 1),
+                            "ms_per_step": ms_solve / args.steps}
+    if ms32 >= ms64:
+        avg = ms32 / n32
+        achieved = bytes_per_pass / (avg * 1e-3) / 1e9
+        roof = {"kernel": "irls_pass_kernel<NT,fp32 Hessian>", "bound": "hbm",
+                "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                "algorithmic_bytes_per_launch": bytes_per_pass, "avg_launch_ms": avg}
+    else:
+        avg = ms64 / n64
+        achieved = mfma_flops_per_pass / (avg * 1e-3) / 1e12
+        roof = {"kernel": "irls_pass_kernel<NT,fp64 Hessian>", "bound": "mfma",
+                "achieved": achieved, "peak": FP64_MFMA_PEAK_TF, "unit": "TFLOP/s",
+                "frac": achieved / FP64_MFMA_PEAK_TF, "traffic": None,
+                "mfma_flops_per_launch": mfma_flops_per_pass, "avg_launch_ms": avg}
+    pmc_file = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc_file):
+        try:
+            pmc = json.load(open(pmc_file))
+            key = "fp32" if roof["bound"] == "hbm" else "fp64"
+            if key in pmc and pmc[key].get("p") == p and pmc[key].get("n") == n:
+                roof["traffic"] = pmc[key]["hbm_bytes_per_launch"]
+        except Exception:
+            pass
+
+    out = {
+        "metric": METRIC, "value": value, "unit": "rows/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic: X~U(-1/2,1/2), beta*=1 on first floor(0.4p) cols, y~Bernoulli"
+                "(sigmoid(X beta*)); counter-based generator in HBM (not timed)",
+        "config": {"workload": f"config2: synthetic logistic n={n:.0e} rows/GPU, p={p}, "
+                               f"K={K} partitions/GPU, fp64 batched IRLS + DLSA combine + LARS/DBIC",
+                   "n_rows_per_gpu": n, "p": p, "partitions_per_gpu": K,
+                   "hessian": args.hessian, "tol": args.tol,
+                   "parallelism": f"dp{world} (partitions sharded; 1 RCCL all-reduce of P^2+2P+1 fp64)"},
+        "roofline": roof,
+        "kernels": kern,
+        "newton": {"iterations": stats_acc[-1]["iterations"],
+                   "passes_fp32": stats_acc[-1]["passes_fp32"],
+                   "passes_fp64": stats_acc[-1]["passes_fp64"],
+                   "n_chunks": stats_acc[-1]["n_chunks"],
+                   "status": fit.status_counts()},
+        "dbic_support_size": int(len(support)),
+        "algorithmic": {"bytes_per_pass": bytes_per_pass, "flops_per_pass": alg_flops_per_pass},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        workers = min(16, os.cpu_count() or 1)
+        out["cpu_baseline"] = cpu_baseline(97656, p, args.cpu_parts, workers)
+        out["vs_cpu_baseline"] = value / out["cpu_baseline"]["value"]
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

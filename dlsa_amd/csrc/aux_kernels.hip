@@ -1,0 +1,137 @@
+// Small kernels around the fused pass: fit state init/finalise, the local
+// partition reduction (dlsa/dlsa.py:30-34 group-sum, done in HBM before the
+// RCCL all-reduce) and the synthetic data generator.
+#include <math.h>
+
+#include "dlsa_internal.hpp"
+
+namespace dlsa {
+
+__global__ void fit_init_kernel(const int64_t* offsets, int K, int P, int start_phase,
+                                double* theta, int32_t* phase, int32_t* backtracks,
+                                int32_t* iters, int32_t* status, double* ll_prev,
+                                double* sig_inv, double* loglik) {
+  const int k = blockIdx.x;
+  const bool empty = offsets[k + 1] <= offsets[k];
+  for (int f = threadIdx.x; f < P; f += blockDim.x) theta[(int64_t)k * P + f] = 0.0;
+  for (int e = threadIdx.x; e < P * P; e += blockDim.x) sig_inv[(int64_t)k * P * P + e] = 0.0;
+  if (threadIdx.x == 0) {
+    phase[k] = empty ? PHASE_DONE : start_phase;
+    backtracks[k] = 0;
+    iters[k] = 0;
+    status[k] = empty ? DLSA_STATUS_EMPTY : STATUS_RUNNING;
+    ll_prev[k] = -INFINITY;
+    loglik[k] = 0.0;
+  }
+}
+
+hipError_t launch_fit_init(const int64_t* offsets_dev, int K, int P, int start_phase,
+                           double* theta, int32_t* phase, int32_t* backtracks, int32_t* iters,
+                           int32_t* status, double* ll_prev, double* sig_inv, double* loglik,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(fit_init_kernel, dim3(K), dim3(256), 0, s, offsets_dev, K, P, start_phase,
+                     theta, phase, backtracks, iters, status, ll_prev, sig_inv, loglik);
+  return hipGetLastError();
+}
+
+// sig_inv_theta = Sig_inv @ theta (models.py:131); still-running -> MAXITER.
+__global__ void fit_finalize_kernel(int K, int P, const double* theta, const double* sig_inv,
+                                    double* sig_inv_theta, int32_t* status) {
+  const int k = blockIdx.x;
+  const double* S = sig_inv + (int64_t)k * P * P;
+  const double* th = theta + (int64_t)k * P;
+  for (int i = threadIdx.x; i < P; i += blockDim.x) {
+    double acc = 0.0;
+    for (int j = 0; j < P; ++j) acc = fma(S[(int64_t)i * P + j], th[j], acc);
+    sig_inv_theta[(int64_t)k * P + i] = acc;
+  }
+  if (threadIdx.x == 0 && status[k] == STATUS_RUNNING) status[k] = DLSA_STATUS_MAXITER;
+}
+
+hipError_t launch_fit_finalize(int K, int P, const double* theta, const double* sig_inv,
+                               double* sig_inv_theta, int32_t* status, hipStream_t s) {
+  hipLaunchKernelGGL(fit_finalize_kernel, dim3(K), dim3(128), 0, s, K, P, theta, sig_inv,
+                     sig_inv_theta, status);
+  return hipGetLastError();
+}
+
+// out = [sum_k Sig_inv_k | sum_k Sig_inv_k theta_k | sum_k theta_k | K]
+// One thread per output element, partitions summed in index order.
+__global__ void reduce_partitions_kernel(const double* sig_inv, const double* sig_inv_theta,
+                                         const double* theta, int K, int P, double* out) {
+  const int64_t PP2 = (int64_t)P * P;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < PP2) {
+    double s = 0.0;
+    for (int k = 0; k < K; ++k) s += sig_inv[(int64_t)k * PP2 + e];
+    out[e] = s;
+  } else if (e < PP2 + P) {
+    const int i = (int)(e - PP2);
+    double s = 0.0;
+    for (int k = 0; k < K; ++k) s += sig_inv_theta[(int64_t)k * P + i];
+    out[e] = s;
+  } else if (e < PP2 + 2 * P) {
+    const int i = (int)(e - PP2 - P);
+    double s = 0.0;
+    for (int k = 0; k < K; ++k) s += theta[(int64_t)k * P + i];
+    out[e] = s;
+  } else if (e == PP2 + 2 * P) {
+    out[e] = (double)K;
+  }
+}
+
+hipError_t launch_reduce_partitions(const double* sig_inv, const double* sig_inv_theta,
+                                    const double* theta, int K, int P, double* out,
+                                    hipStream_t s) {
+  const int64_t n = (int64_t)P * P + 2 * P + 1;
+  const int threads = 256;
+  const int blocks = (int)((n + threads - 1) / threads);
+  hipLaunchKernelGGL(reduce_partitions_kernel, dim3(blocks), dim3(threads), 0, s, sig_inv,
+                     sig_inv_theta, theta, K, P, out);
+  return hipGetLastError();
+}
+
+// ---- synthetic data: counter-based splitmix64 streams -----------------------
+// X[i, j] = u(seed, (row0 + i) * p + j) - 0.5, y[i] = u(seed ^ kYSalt, row0 + i) <
+// sigmoid(sum_{j < floor(0.4 p)} X[i, j]).  oracle/dlsa_oracle.py:simulate_counter
+// restates it bit for bit.
+__device__ __forceinline__ double u01(uint64_t seed, uint64_t ctr) {
+  uint64_t z = seed + (ctr + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (double)(z >> 11) * 0x1.0p-53;
+}
+constexpr uint64_t kYSalt = 0x5DEECE66Dull;
+
+__global__ void simulate_x_kernel(double* X, int64_t n, int p, uint64_t seed, int64_t row0) {
+  const int64_t total = n * p;
+  const int64_t base = row0 * p;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x)
+    X[e] = u01(seed, (uint64_t)(base + e)) - 0.5;
+}
+
+__global__ void simulate_y_kernel(const double* X, double* y, int64_t n, int p, uint64_t seed,
+                                  int64_t row0) {
+  const int p1 = (int)(p * 0.4);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    double eta = 0.0;
+    for (int j = 0; j < p1; ++j) eta = eta + X[i * p + j];
+    const double prob = 1.0 / (1.0 + exp(-eta));
+    y[i] = u01(seed ^ kYSalt, (uint64_t)(row0 + i)) < prob ? 1.0 : 0.0;
+  }
+}
+
+hipError_t launch_simulate(double* X, double* y, int64_t n, int p, uint64_t seed, int64_t row0,
+                           hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(simulate_x_kernel, dim3(8192), dim3(256), 0, s, X, n, p, seed, row0);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(simulate_y_kernel, dim3(4096), dim3(256), 0, s, X, y, n, p, seed, row0);
+  return hipGetLastError();
+}
+
+}  // namespace dlsa

@@ -1,0 +1,430 @@
+// extern "C" entry points of libdlsa_hip.so (declared in include/dlsa_hip.h)
+// and the host side of the batched Newton/IRLS driver.
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "dlsa_internal.hpp"
+
+namespace dlsa {
+
+static thread_local std::string g_last_error;
+static thread_local dlsa_fit_stats g_stats;
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+#define DLSA_HIP_TRY(expr)                                                            \
+  do {                                                                                \
+    hipError_t _e = (expr);                                                           \
+    if (_e != hipSuccess) {                                                           \
+      set_error(std::string(#expr) + ": " + hipGetErrorString(_e));                   \
+      return DLSA_E_HIP;                                                              \
+    }                                                                                 \
+  } while (0)
+
+static inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
+
+// Chunking: each wave streams a run of consecutive rows of one partition.
+// Enough chunks to give every CU several waves, few enough that the partial
+// tiles (T*2 KiB per chunk) stay ~1-2% of the X traffic.
+struct Plan {
+  int P = 0, NT = 0, T = 0, PP = 0;
+  int n_chunks = 0;
+  std::vector<int64_t> chunk_row0;
+  std::vector<int32_t> chunk_rows, chunk_part, part_chunk_begin;
+};
+
+static int auto_rows_per_chunk(int64_t n_total) {
+  // target ~8 waves per CU-slot round on 256 CUs
+  int64_t r = n_total / 4096;
+  r = std::max<int64_t>(256, std::min<int64_t>(r, 8192));
+  return (int)r;
+}
+
+static bool make_plan(const int64_t* offsets, int K, int p, int intercept, int rows_per_chunk,
+                      Plan& pl) {
+  pl.P = p + (intercept ? 1 : 0);
+  pl.NT = (pl.P + 15) / 16;
+  pl.T = pl.NT * (pl.NT + 1) / 2;
+  pl.PP = 16 * pl.NT;
+  const int64_t n_total = offsets[K];
+  const int rpc = rows_per_chunk > 0 ? rows_per_chunk : auto_rows_per_chunk(n_total);
+  pl.part_chunk_begin.assign(K + 1, 0);
+  pl.chunk_row0.clear();
+  pl.chunk_rows.clear();
+  pl.chunk_part.clear();
+  for (int k = 0; k < K; ++k) {
+    pl.part_chunk_begin[k] = (int32_t)pl.chunk_row0.size();
+    const int64_t a = offsets[k], b = offsets[k + 1];
+    const int64_t n = b - a;
+    if (n <= 0) continue;
+    const int64_t nc = (n + rpc - 1) / rpc;
+    for (int64_t c = 0; c < nc; ++c) {
+      const int64_t r0 = a + n * c / nc, r1 = a + n * (c + 1) / nc;
+      pl.chunk_row0.push_back(r0);
+      pl.chunk_rows.push_back((int32_t)(r1 - r0));
+      pl.chunk_part.push_back(k);
+    }
+  }
+  pl.part_chunk_begin[K] = (int32_t)pl.chunk_row0.size();
+  pl.n_chunks = (int)pl.chunk_row0.size();
+  return true;
+}
+
+struct Layout {
+  int64_t off_row0, off_rows, off_part, off_pcb, off_offsets;
+  int64_t off_slabH, off_slabg, off_slabll;
+  int64_t off_phase, off_bt, off_llprev, off_thprev, off_dprev, off_counters;
+  int64_t total;
+};
+
+static Layout make_layout(const Plan& pl, int K) {
+  Layout L;
+  int64_t o = 0;
+  auto take = [&](int64_t bytes) {
+    int64_t r = o;
+    o = align_up(o + bytes, 256);
+    return r;
+  };
+  L.off_row0 = take(8LL * std::max(pl.n_chunks, 1));
+  L.off_rows = take(4LL * std::max(pl.n_chunks, 1));
+  L.off_part = take(4LL * std::max(pl.n_chunks, 1));
+  L.off_pcb = take(4LL * (K + 1));
+  L.off_offsets = take(8LL * (K + 1));
+  L.off_slabH = take(8LL * std::max(pl.n_chunks, 1) * pl.T * 256);
+  L.off_slabg = take(8LL * std::max(pl.n_chunks, 1) * pl.PP);
+  L.off_slabll = take(8LL * std::max(pl.n_chunks, 1));
+  L.off_phase = take(4LL * K);
+  L.off_bt = take(4LL * K);
+  L.off_llprev = take(8LL * K);
+  L.off_thprev = take(8LL * K * pl.P);
+  L.off_dprev = take(8LL * K * pl.P);
+  L.off_counters = take(16);
+  L.total = o;
+  return L;
+}
+
+static int check_offsets(const int64_t* offsets, int K) {
+  if (!offsets || K < 1) {
+    set_error("offsets must be a host array of K+1 >= 2 entries");
+    return DLSA_E_INVALID;
+  }
+  if (offsets[0] != 0) {
+    set_error("offsets[0] must be 0");
+    return DLSA_E_INVALID;
+  }
+  for (int k = 0; k < K; ++k)
+    if (offsets[k + 1] < offsets[k]) {
+      set_error("offsets must be non-decreasing");
+      return DLSA_E_INVALID;
+    }
+  for (int k = 0; k < K; ++k)
+    if (offsets[k + 1] - offsets[k] > (int64_t)INT32_MAX) {
+      set_error("a partition holds more than 2^31-1 rows");
+      return DLSA_E_INVALID;
+    }
+  return DLSA_OK;
+}
+
+}  // namespace dlsa
+
+using namespace dlsa;
+
+extern "C" {
+
+void dlsa_fit_options_default(dlsa_fit_options* opt) {
+  if (!opt) return;
+  memset(opt, 0, sizeof(*opt));
+  opt->hessian_mode = DLSA_HESSIAN_MIXED;
+  opt->switch_tol = 1e-6;
+}
+
+const char* dlsa_last_error(void) { return g_last_error.c_str(); }
+
+const char* dlsa_build_info(void) {
+  return "libdlsa_hip gfx950 (CDNA4): fused IRLS pass (LDS-DMA ring, f64/f32 16x16x4 MFMA), "
+         "LDS Cholesky Newton update, host LARS";
+}
+
+int64_t dlsa_logistic_workspace_bytes(const int64_t* offsets, int32_t K, int32_t p,
+                                      int32_t fit_intercept, int32_t rows_per_chunk) {
+  if (check_offsets(offsets, K) != DLSA_OK) return -1;
+  Plan pl;
+  make_plan(offsets, K, p, fit_intercept, rows_per_chunk, pl);
+  return make_layout(pl, K).total;
+}
+
+int dlsa_last_fit_stats(dlsa_fit_stats* out) {
+  if (!out) return DLSA_E_INVALID;
+  *out = g_stats;
+  return DLSA_OK;
+}
+
+int dlsa_logistic_fit_batched_ex(const double* X, const double* y, const int64_t* offsets,
+                                 int32_t K, int32_t p, int32_t fit_intercept,
+                                 const double* center, const double* scale, int32_t max_iter,
+                                 double tol, double* theta, double* sig_inv,
+                                 double* sig_inv_theta, double* loglik, int32_t* iters,
+                                 int32_t* status, const dlsa_fit_options* opt_in,
+                                 void* stream_) {
+  const auto t_start = std::chrono::steady_clock::now();
+  g_last_error.clear();
+  memset(&g_stats, 0, sizeof(g_stats));
+  hipStream_t stream = (hipStream_t)stream_;
+  dlsa_fit_options opt;
+  if (opt_in)
+    opt = *opt_in;
+  else
+    dlsa_fit_options_default(&opt);
+  if (opt.switch_tol <= 0) opt.switch_tol = 1e-6;
+
+  int rc = check_offsets(offsets, K);
+  if (rc != DLSA_OK) return rc;
+  if (p < 0 || (p == 0 && !fit_intercept)) {
+    set_error("p must be >= 1 (or 0 with an intercept)");
+    return DLSA_E_INVALID;
+  }
+  const int P = p + (fit_intercept ? 1 : 0);
+  if (P > DLSA_MAX_P_FUSED) {
+    set_error("P = p + intercept > " + std::to_string(DLSA_MAX_P_FUSED) +
+              " is not supported by the fused pass yet");
+    return DLSA_E_UNSUPPORTED;
+  }
+  if ((center == nullptr) != (scale == nullptr)) {
+    set_error("center and scale must both be given or both be NULL");
+    return DLSA_E_INVALID;
+  }
+  if (!theta || !sig_inv || !sig_inv_theta || !loglik || !iters || !status) {
+    set_error("null output pointer");
+    return DLSA_E_INVALID;
+  }
+  const int64_t n_total = offsets[K];
+  if (n_total > 0 && (!X || !y)) {
+    set_error("null X or y");
+    return DLSA_E_INVALID;
+  }
+  if (max_iter < 1) max_iter = 1;
+  if (!(tol > 0)) tol = 1e-10;
+
+  Plan pl;
+  make_plan(offsets, K, p, fit_intercept, opt.rows_per_chunk, pl);
+  const Layout L = make_layout(pl, K);
+  g_stats.n_chunks = pl.n_chunks;
+
+  char* ws = (char*)opt.workspace;
+  bool owned = false;
+  if (!ws) {
+    DLSA_HIP_TRY(hipMallocAsync((void**)&ws, L.total, stream));
+    owned = true;
+  } else if (opt.workspace_bytes < L.total) {
+    set_error("workspace too small: need " + std::to_string(L.total) + " bytes");
+    return DLSA_E_WORKSPACE;
+  }
+  struct Free {
+    char* p;
+    bool own;
+    hipStream_t s;
+    ~Free() {
+      if (own && p) (void)hipFreeAsync(p, s);
+    }
+  } freer{ws, owned, stream};
+
+  auto at = [&](int64_t off) { return (void*)(ws + off); };
+  int64_t* d_row0 = (int64_t*)at(L.off_row0);
+  int32_t* d_rows = (int32_t*)at(L.off_rows);
+  int32_t* d_part = (int32_t*)at(L.off_part);
+  int32_t* d_pcb = (int32_t*)at(L.off_pcb);
+  int64_t* d_offsets = (int64_t*)at(L.off_offsets);
+  double* slabH = (double*)at(L.off_slabH);
+  double* slabg = (double*)at(L.off_slabg);
+  double* slabll = (double*)at(L.off_slabll);
+  int32_t* d_phase = (int32_t*)at(L.off_phase);
+  int32_t* d_bt = (int32_t*)at(L.off_bt);
+  double* d_llprev = (double*)at(L.off_llprev);
+  double* d_thprev = (double*)at(L.off_thprev);
+  double* d_dprev = (double*)at(L.off_dprev);
+  int32_t* d_cnt = (int32_t*)at(L.off_counters);
+
+  if (pl.n_chunks > 0) {
+    DLSA_HIP_TRY(hipMemcpyAsync(d_row0, pl.chunk_row0.data(), 8LL * pl.n_chunks,
+                                hipMemcpyHostToDevice, stream));
+    DLSA_HIP_TRY(hipMemcpyAsync(d_rows, pl.chunk_rows.data(), 4LL * pl.n_chunks,
+                                hipMemcpyHostToDevice, stream));
+    DLSA_HIP_TRY(hipMemcpyAsync(d_part, pl.chunk_part.data(), 4LL * pl.n_chunks,
+                                hipMemcpyHostToDevice, stream));
+  }
+  DLSA_HIP_TRY(hipMemcpyAsync(d_pcb, pl.part_chunk_begin.data(), 4LL * (K + 1),
+                              hipMemcpyHostToDevice, stream));
+  DLSA_HIP_TRY(hipMemcpyAsync(d_offsets, offsets, 8LL * (K + 1), hipMemcpyHostToDevice, stream));
+
+  const int start_phase = opt.hessian_mode == DLSA_HESSIAN_FP64 ? PHASE_F64 : PHASE_F32;
+  DLSA_HIP_TRY(launch_fit_init(d_offsets, K, P, start_phase, theta, d_phase, d_bt, iters, status,
+                               d_llprev, sig_inv, loglik, stream));
+
+  int n_running[2] = {0, 0};
+  for (int k = 0; k < K; ++k)
+    if (offsets[k + 1] > offsets[k]) n_running[start_phase]++;
+
+  PassArgs pa;
+  memset(&pa, 0, sizeof(pa));
+  pa.X = X;
+  pa.y = y;
+  pa.chunk_row0 = d_row0;
+  pa.chunk_rows = d_rows;
+  pa.chunk_part = d_part;
+  pa.phase = d_phase;
+  pa.theta = theta;
+  pa.center = center;
+  pa.scale = scale;
+  pa.slab_H = slabH;
+  pa.slab_g = slabg;
+  pa.slab_ll = slabll;
+  if (n_total > 0) {
+    const uintptr_t xend = (uintptr_t)(X + n_total * (int64_t)p);
+    pa.x_last16 = ((xend + 15) & ~(uintptr_t)15) - 16;
+    pa.y_last4 = (uintptr_t)(y + n_total) - 4;
+  }
+  pa.p = p;
+  pa.P = P;
+  pa.intercept = fit_intercept ? 1 : 0;
+  pa.slot_bytes = pass_slot_bytes(pl.NT);
+
+  SolveArgs sa;
+  memset(&sa, 0, sizeof(sa));
+  sa.part_chunk_begin = d_pcb;
+  sa.slab_H = slabH;
+  sa.slab_g = slabg;
+  sa.slab_ll = slabll;
+  sa.theta = theta;
+  sa.theta_prev = d_thprev;
+  sa.delta_prev = d_dprev;
+  sa.ll_prev = d_llprev;
+  sa.phase = d_phase;
+  sa.backtracks = d_bt;
+  sa.iters = iters;
+  sa.status = status;
+  sa.counters = d_cnt;
+  sa.sig_inv = sig_inv;
+  sa.loglik = loglik;
+  sa.P = P;
+  sa.NT = pl.NT;
+  sa.tol = tol;
+  sa.switch_tol = opt.switch_tol;
+
+  const bool standardize = center != nullptr;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  if (opt.record_timing) {
+    DLSA_HIP_TRY(hipEventCreate(&ev[0]));
+    DLSA_HIP_TRY(hipEventCreate(&ev[1]));
+  }
+  struct EvFree {
+    hipEvent_t* e;
+    ~EvFree() {
+      if (e[0]) (void)hipEventDestroy(e[0]);
+      if (e[1]) (void)hipEventDestroy(e[1]);
+    }
+  } evfree{ev};
+  auto timed = [&](double* acc, auto&& launch) -> hipError_t {
+    if (!opt.record_timing) return launch();
+    hipError_t e = hipEventRecord(ev[0], stream);
+    if (e != hipSuccess) return e;
+    e = launch();
+    if (e != hipSuccess) return e;
+    e = hipEventRecord(ev[1], stream);
+    if (e != hipSuccess) return e;
+    e = hipEventSynchronize(ev[1]);
+    if (e != hipSuccess) return e;
+    float ms = 0.f;
+    e = hipEventElapsedTime(&ms, ev[0], ev[1]);
+    *acc += ms;
+    return e;
+  };
+
+  int32_t* h_cnt = nullptr;
+  DLSA_HIP_TRY(hipHostMalloc((void**)&h_cnt, 16, hipHostMallocDefault));
+  struct HFree {
+    int32_t* p;
+    ~HFree() {
+      if (p) (void)hipHostFree(p);
+    }
+  } hfree{h_cnt};
+
+  int it = 0;
+  for (; it < max_iter && (n_running[0] + n_running[1]) > 0 && pl.n_chunks > 0; ++it) {
+    for (int ph = 0; ph < 2; ++ph) {
+      if (n_running[ph] == 0) continue;
+      const bool f64 = ph == PHASE_F64;
+      pa.want_phase = ph;
+      const int waves = pass_waves_per_cu(f64);
+      int nslot = (160 * 1024 / waves) / pa.slot_bytes;
+      nslot = std::max(2, std::min(nslot, 4));
+      pa.nslot = nslot;
+      DLSA_HIP_TRY(timed(f64 ? &g_stats.ms_pass_fp64 : &g_stats.ms_pass_fp32, [&] {
+        return launch_irls_pass(pa, pl.NT, f64, standardize, pl.n_chunks, stream);
+      }));
+      if (f64) {
+        g_stats.passes_fp64++;
+      } else {
+        g_stats.passes_fp32++;
+      }
+    }
+    DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
+    DLSA_HIP_TRY(timed(&g_stats.ms_solve, [&] { return launch_newton_solve(sa, K, stream); }));
+    DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, stream));
+    DLSA_HIP_TRY(hipStreamSynchronize(stream));
+    n_running[0] = h_cnt[0];
+    n_running[1] = h_cnt[1];
+  }
+  g_stats.iterations = it;
+  // rows streamed per pass kind (all chunks are launched; idle ones exit)
+  g_stats.rows_fp32 = (int64_t)g_stats.passes_fp32 * n_total;
+  g_stats.rows_fp64 = (int64_t)g_stats.passes_fp64 * n_total;
+
+  DLSA_HIP_TRY(launch_fit_finalize(K, P, theta, sig_inv, sig_inv_theta, status, stream));
+  DLSA_HIP_TRY(hipStreamSynchronize(stream));
+  g_stats.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() -
+                                                               t_start)
+                         .count();
+  return DLSA_OK;
+}
+
+int dlsa_logistic_fit_batched(const double* X, const double* y, const int64_t* offsets,
+                              int32_t K, int32_t p, int32_t fit_intercept, const double* center,
+                              const double* scale, int32_t max_iter, double tol, double* theta,
+                              double* sig_inv, double* sig_inv_theta, double* loglik,
+                              int32_t* iters, int32_t* status, void* stream) {
+  return dlsa_logistic_fit_batched_ex(X, y, offsets, K, p, fit_intercept, center, scale,
+                                      max_iter, tol, theta, sig_inv, sig_inv_theta, loglik,
+                                      iters, status, nullptr, stream);
+}
+
+int dlsa_reduce_partitions(const double* sig_inv, const double* sig_inv_theta,
+                           const double* theta, int32_t K, int32_t p, double* out,
+                           void* stream) {
+  g_last_error.clear();
+  if (K < 1 || p < 1 || !sig_inv || !sig_inv_theta || !theta || !out) {
+    set_error("dlsa_reduce_partitions: invalid arguments");
+    return DLSA_E_INVALID;
+  }
+  DLSA_HIP_TRY(launch_reduce_partitions(sig_inv, sig_inv_theta, theta, K, p, out,
+                                        (hipStream_t)stream));
+  return DLSA_OK;
+}
+
+int dlsa_simulate_logistic(double* X, double* y, int64_t n, int32_t p, uint64_t seed,
+                           int64_t row0, void* stream) {
+  g_last_error.clear();
+  if (n < 0 || p < 1 || (n > 0 && (!X || !y))) {
+    set_error("dlsa_simulate_logistic: invalid arguments");
+    return DLSA_E_INVALID;
+  }
+  DLSA_HIP_TRY(launch_simulate(X, y, n, p, seed, row0, (hipStream_t)stream));
+  return DLSA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,89 @@
+// Internal declarations shared by the HIP translation units of libdlsa_hip.so.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/dlsa_hip.h"
+
+namespace dlsa {
+
+// Per-partition Newton phase.  MIXED fits start in PHASE_F32 (fp32-MFMA
+// Hessian, fp64 gradient) and switch to PHASE_F64 for the pass whose Hessian
+// is returned as Sig_inv; FP64 fits start in PHASE_F64.
+enum : int32_t { PHASE_F32 = 0, PHASE_F64 = 1, PHASE_DONE = 2 };
+enum : int32_t { STATUS_RUNNING = -1 };
+
+// Rows of X one wave stages per LDS slot (4 MFMA k-steps of 4 rows).
+constexpr int kRowsPerBlock = 8;
+
+// Arguments of the fused IRLS pass (one wave = one chunk of one partition).
+struct PassArgs {
+  const double* X;            // [n_total, p]
+  const double* y;            // [n_total]
+  const int64_t* chunk_row0;  // [n_chunks] first global row of the chunk
+  const int32_t* chunk_rows;  // [n_chunks]
+  const int32_t* chunk_part;  // [n_chunks]
+  const int32_t* phase;       // [K]
+  const double* theta;        // [K, P] current iterate
+  const double* center;       // [p] or null
+  const double* scale;        // [p] or null
+  double* slab_H;             // [n_chunks, T, 16, 16] partial X^T W X tiles
+  double* slab_g;             // [n_chunks, 16*NT] partial X^T (y - mu)
+  double* slab_ll;            // [n_chunks] partial log-likelihood
+  uintptr_t x_last16;         // last 16-B aligned address whose 16 B are readable
+  uintptr_t y_last4;          // last 4-B address inside y
+  int32_t p;                  // columns of X
+  int32_t P;                  // p + intercept
+  int32_t intercept;
+  int32_t want_phase;
+  int32_t nslot;              // LDS ring depth (slots of kRowsPerBlock rows)
+  int32_t slot_bytes;
+};
+
+// Arguments of the per-partition Newton update.
+struct SolveArgs {
+  const int32_t* part_chunk_begin;  // [K+1]
+  const double* slab_H;
+  const double* slab_g;
+  const double* slab_ll;
+  double* theta;        // [K, P] (in/out: the iterate, returned as coef)
+  double* theta_prev;   // [K, P]
+  double* delta_prev;   // [K, P]
+  double* ll_prev;      // [K]
+  int32_t* phase;       // [K]
+  int32_t* backtracks;  // [K]
+  int32_t* iters;       // [K]
+  int32_t* status;      // [K]
+  int32_t* counters;    // [2] partitions still running per phase
+  double* sig_inv;      // [K, P, P] out
+  double* loglik;       // [K] out
+  int32_t P;
+  int32_t NT;
+  double tol;
+  double switch_tol;
+};
+
+// Launchers (defined in the .hip files).
+hipError_t launch_irls_pass(const PassArgs& a, int NT, bool f64, bool standardize,
+                            int n_chunks, hipStream_t s);
+int pass_slot_bytes(int NT);
+int pass_waves_per_cu(bool f64);
+hipError_t launch_newton_solve(const SolveArgs& a, int K, hipStream_t s);
+hipError_t launch_fit_init(const int64_t* offsets_dev, int K, int P, int start_phase,
+                           double* theta, int32_t* phase, int32_t* backtracks,
+                           int32_t* iters, int32_t* status, double* ll_prev,
+                           double* sig_inv, double* loglik, hipStream_t s);
+hipError_t launch_fit_finalize(int K, int P, const double* theta, const double* sig_inv,
+                               double* sig_inv_theta, int32_t* status, hipStream_t s);
+hipError_t launch_reduce_partitions(const double* sig_inv, const double* sig_inv_theta,
+                                    const double* theta, int K, int P, double* out,
+                                    hipStream_t s);
+hipError_t launch_simulate(double* X, double* y, int64_t n, int p, uint64_t seed,
+                           int64_t row0, hipStream_t s);
+
+void set_error(const std::string& msg);
+
+}  // namespace dlsa

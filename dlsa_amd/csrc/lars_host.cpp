@@ -1,0 +1,291 @@
+// Host LARS / adaptive-lasso path on the LSA quadratic form.
+//
+// Behavioural spec: dlsa/lsa.py:90-212 (the Python port of R lars.lsa that
+// dlsa/dlsa.py:77-80 calls).  The path is a LAR / LASSO homotopy on the
+// quadratic loss (b - beta)^T Sigma (b - beta) after the adaptive rescaling
+// Sigma <- D Sigma D, b <- sign(b), D = diag|b0| (lsa.py:108-109), with an
+// incrementally updated Cholesky factor R of the active Gram block
+// (lsa.py:12-32 update, lsa.py:35-80 Givens downdate).  Each knot reports
+// RSS_k, BIC = RSS + log(n) dof (the DBIC of the paper) and AIC = RSS + 2 dof
+// (lsa.py:190-211).
+//
+// Reference defects fixed: the intercept branch uses the
+// parameter count (lsa.py:100 used the sample size n and raises IndexError);
+// the singular back-out keeps the leading block of R (lsa.py:141-142 indexed
+// a diagonal).  A knot's "C" vector for the step length is taken over the
+// columns that are neither active nor ignored, which is what lsa.py:157-161
+// computes whenever no variable has been ignored.
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/dlsa_hip.h"
+
+namespace dlsa {
+void set_error(const std::string& msg);
+}
+
+namespace {
+
+struct Chol {
+  // upper-triangular R (d x d) stored with leading dimension m
+  int m = 0, d = 0;
+  std::vector<double> r;
+  explicit Chol(int m_) : m(m_), d(0), r((size_t)m_ * m_, 0.0) {}
+  double& at(int i, int j) { return r[(size_t)i * m + j]; }
+  double at(int i, int j) const { return r[(size_t)i * m + j]; }
+  // solve R^T x = b (forward)
+  void solve_rt(const double* b, double* x) const {
+    for (int i = 0; i < d; ++i) {
+      double s = b[i];
+      for (int k = 0; k < i; ++k) s -= at(k, i) * x[k];
+      x[i] = s / at(i, i);
+    }
+  }
+  // solve R x = b (backward)
+  void solve_r(const double* b, double* x) const {
+    for (int i = d - 1; i >= 0; --i) {
+      double s = b[i];
+      for (int k = i + 1; k < d; ++k) s -= at(i, k) * x[k];
+      x[i] = s / at(i, i);
+    }
+  }
+};
+
+}  // namespace
+
+extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
+                             int32_t intercept, double n, int32_t type, double eps,
+                             int32_t max_steps, double* beta_out, double* beta0_out,
+                             double* aic, double* bic, int32_t* n_steps) {
+  using dlsa::set_error;
+  if (!Sigma0 || !b0 || P < 1 + (intercept ? 1 : 0) || !beta_out || !beta0_out || !aic || !bic ||
+      !n_steps) {
+    set_error("dlsa_lars_lsa: invalid arguments");
+    return DLSA_E_INVALID;
+  }
+  const bool lasso = type == 1;
+  if (!(eps > 0)) eps = 2.220446049250313e-16;
+  const int ic = intercept ? 1 : 0;
+  const int m = P - ic;
+  if (max_steps <= 0) max_steps = 8 * m;
+
+  // quadratic form after removing the intercept (Schur complement)
+  std::vector<double> Sig((size_t)m * m), b(m), a12(ic ? m : 0);
+  double a11 = 1.0, beta0_init = 0.0;
+  if (ic) {
+    a11 = Sigma0[0];
+    for (int i = 0; i < m; ++i) a12[i] = Sigma0[(size_t)(i + 1) * P];
+    for (int i = 0; i < m; ++i)
+      for (int j = 0; j < m; ++j)
+        Sig[(size_t)i * m + j] = Sigma0[(size_t)(i + 1) * P + (j + 1)] - a12[i] * a12[j] / a11;
+    for (int i = 0; i < m; ++i) b[i] = b0[i + 1];
+    double s = 0;
+    for (int i = 0; i < m; ++i) s += a12[i] * b[i];
+    beta0_init = s / a11;
+  } else {
+    for (size_t e = 0; e < (size_t)m * m; ++e) Sig[e] = Sigma0[e];
+    for (int i = 0; i < m; ++i) b[i] = b0[i];
+  }
+  std::vector<double> absb(m), sgnb(m);
+  for (int i = 0; i < m; ++i) {
+    absb[i] = fabs(b[i]);
+    sgnb[i] = (b[i] > 0) - (b[i] < 0);
+  }
+  for (int i = 0; i < m; ++i)
+    for (int j = 0; j < m; ++j) Sig[(size_t)i * m + j] *= absb[i] * absb[j];
+  auto S = [&](int i, int j) { return Sig[(size_t)i * m + j]; };
+
+  std::vector<double> Cvec(m, 0.0);
+  for (int j = 0; j < m; ++j) {
+    double s = 0;
+    for (int i = 0; i < m; ++i) s += sgnb[i] * S(i, j);
+    Cvec[j] = s;
+  }
+
+  const size_t rows = (size_t)max_steps + 1;
+  memset(beta_out, 0, sizeof(double) * rows * m);
+  auto B = [&](int k, int j) -> double& { return beta_out[(size_t)k * m + j]; };
+
+  std::vector<int> active, ignores;
+  std::vector<double> Sign;
+  std::vector<char> in_active(m, 0), in_ignores(m, 0);
+  std::vector<char> drops;  // per active position, from the last lasso step
+  bool any_drop = false;
+  Chol R(m);
+  int rank = 0;
+  int k = 0;
+  std::vector<double> C, u, Gi1, w, a;
+  std::vector<int> inactive, keep;
+
+  while (k < max_steps && (int)active.size() < m) {
+    ++k;
+    inactive.clear();
+    for (int j = 0; j < m; ++j)
+      if (!in_active[j]) inactive.push_back(j);
+    double Cmax = 0;
+    for (int j : inactive) Cmax = std::max(Cmax, fabs(Cvec[j]));
+    if (!any_drop) {
+      for (int j : inactive) {
+        if (!(fabs(Cvec[j]) >= Cmax - eps)) continue;
+        // add variable j: extend R by the column [R^-T Sigma_A,j ; rpp]
+        const int da = R.d;
+        if (da == 0) {
+          R.d = 1;
+          R.at(0, 0) = sqrt(S(j, j));
+          rank = 1;
+        } else {
+          std::vector<double> xold(da), rcol(da);
+          for (int q = 0; q < da; ++q) xold[q] = S(j, active[q]);
+          R.solve_rt(xold.data(), rcol.data());
+          double rpp = S(j, j);
+          for (int q = 0; q < da; ++q) rpp -= rcol[q] * rcol[q];
+          if (rpp <= eps) {
+            rpp = eps;
+          } else {
+            rpp = sqrt(rpp);
+            ++rank;
+          }
+          for (int q = 0; q < da; ++q) R.at(q, da) = rcol[q];
+          for (int q = 0; q < da; ++q) R.at(da, q) = 0.0;
+          R.at(da, da) = rpp;
+          R.d = da + 1;
+        }
+        if (rank == (int)active.size()) {  // singular: back out, ignore j
+          R.d = (int)active.size();
+          ignores.push_back(j);
+          in_ignores[j] = 1;
+        } else {
+          active.push_back(j);
+          in_active[j] = 1;
+          Sign.push_back((Cvec[j] > 0) - (Cvec[j] < 0));
+        }
+      }
+    }
+    const int na = (int)active.size();
+    if (na == 0) break;
+    // Gi1 = (R^T R)^-1 Sign ; A = 1/sqrt(Sign . Gi1) ; w = A Gi1
+    u.assign(na, 0.0);
+    Gi1.assign(na, 0.0);
+    R.solve_rt(Sign.data(), u.data());
+    R.solve_r(u.data(), Gi1.data());
+    double sg = 0;
+    for (int q = 0; q < na; ++q) sg += Gi1[q] * Sign[q];
+    const double A = 1.0 / sqrt(sg);
+    w.assign(na, 0.0);
+    for (int q = 0; q < na; ++q) w[q] = A * Gi1[q];
+    double gamhat = Cmax / A;
+    if (na < m) {
+      keep.clear();
+      for (int j = 0; j < m; ++j)
+        if (!in_active[j] && !in_ignores[j]) keep.push_back(j);
+      for (int j : keep) {
+        double aj = 0;
+        for (int q = 0; q < na; ++q) aj += w[q] * S(active[q], j);
+        const double c = Cvec[j];
+        const double g1 = (Cmax - c) / (A - aj), g2 = (Cmax + c) / (A + aj);
+        if (g1 > eps) gamhat = std::min(gamhat, g1);
+        if (g2 > eps) gamhat = std::min(gamhat, g2);
+      }
+    }
+    any_drop = false;
+    drops.assign(na, 0);
+    if (lasso) {
+      double zmin = gamhat;
+      std::vector<double> z1(na);
+      for (int q = 0; q < na; ++q) {
+        z1[q] = -B(k - 1, active[q]) / w[q];
+        if (z1[q] > eps) zmin = std::min(zmin, z1[q]);
+      }
+      if (zmin < gamhat) {
+        gamhat = zmin;
+        for (int q = 0; q < na; ++q) drops[q] = z1[q] == zmin;
+        any_drop = true;
+      }
+    }
+    for (int j = 0; j < m; ++j) B(k, j) = B(k - 1, j);
+    for (int q = 0; q < na; ++q) B(k, active[q]) += gamhat * w[q];
+    for (int j = 0; j < m; ++j) {
+      double s = 0;
+      for (int q = 0; q < na; ++q) s += S(j, active[q]) * w[q];
+      Cvec[j] -= gamhat * s;
+    }
+    if (lasso && any_drop) {
+      for (int q = na - 1; q >= 0; --q) {
+        if (!drops[q]) continue;
+        // downdate: delete column q of R, re-triangularise with Givens
+        const int d = R.d;
+        if (d == 1) {
+          R.d = 0;
+          continue;
+        }
+        for (int i = 0; i < d; ++i)
+          for (int c = q; c < d - 1; ++c) R.at(i, c) = R.at(i, c + 1);
+        for (int i = q + 1; i < d; ++i) {
+          const double aa = R.at(i - 1, i - 1), bb = R.at(i, i - 1);
+          if (bb == 0) continue;
+          double c, s;
+          if (!(fabs(bb) > fabs(aa))) {
+            const double tau = -bb / aa;
+            c = 1 / sqrt(1 + tau * tau);
+            s = c * tau;
+          } else {
+            const double tau = -aa / bb;
+            s = 1 / sqrt(1 + tau * tau);
+            c = s * tau;
+          }
+          for (int col = i - 1; col < d - 1; ++col) {
+            const double x1 = R.at(i - 1, col), x2 = R.at(i, col);
+            R.at(i - 1, col) = c * x1 - s * x2;
+            R.at(i, col) = s * x1 + c * x2;
+          }
+        }
+        for (int col = 0; col < d; ++col) R.at(d - 1, col) = 0.0;
+        R.d = d - 1;
+      }
+      rank = R.d;
+      std::vector<int> na_active;
+      std::vector<double> na_sign;
+      for (int q = 0; q < na; ++q) {
+        if (drops[q]) {
+          B(k, active[q]) = 0.0;
+          in_active[active[q]] = 0;
+        } else {
+          na_active.push_back(active[q]);
+          na_sign.push_back(Sign[q]);
+        }
+      }
+      active.swap(na_active);
+      Sign.swap(na_sign);
+    }
+  }
+
+  const int nst = k + 1;
+  *n_steps = nst;
+  const double logn = log(n);
+  std::vector<double> dff(m), tmp(m);
+  for (int s = 0; s < nst; ++s) {
+    for (int j = 0; j < m; ++j) dff[j] = sgnb[j] - B(s, j);
+    double rss = 0;
+    for (int i = 0; i < m; ++i) {
+      double t = 0;
+      for (int j = 0; j < m; ++j) t += S(i, j) * dff[j];
+      rss += dff[i] * t;
+    }
+    int dof = 0;
+    double b0s = beta0_init;
+    for (int j = 0; j < m; ++j) {
+      const double v = B(s, j) * absb[j];
+      B(s, j) = v;
+      if (fabs(v) > eps) ++dof;
+      if (ic) b0s -= a12[j] * v / a11;
+    }
+    beta0_out[s] = ic ? b0s : 0.0;
+    bic[s] = rss + logn * dof;
+    aic[s] = rss + 2.0 * dof;
+  }
+  return DLSA_OK;
+}

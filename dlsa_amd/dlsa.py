@@ -1,0 +1,119 @@
+"""Combine and selection steps of DLSA (drop-in for dlsa/dlsa.py).
+
+* ``dlsa_mapred`` -- dlsa/dlsa.py:21-61: sum the per-partition outputs,
+  WLSE = lstsq(sum Sig_inv, sum Sig_inv theta), ONESHOT = sum theta / K.  For
+  a GPU ``BatchedFit`` the sum runs in HBM (``dlsa_reduce_partitions``); the
+  pandas forms mirror the Spark ``groupby('par_id').sum()``.
+* ``dlsa`` -- dlsa/dlsa.py:70-100: adaptive-lasso LSA path and the AIC / BIC
+  (DBIC) argmin, through the native ``lars_lsa`` instead of R via rpy2.
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _hip
+
+
+def _frame(S, v, sum_theta, K, columns):
+    import pandas as pd
+
+    p = v.size
+    beta_ols = np.linalg.lstsq(S, v, rcond=None)[0]          # dlsa.py:48-49
+    beta_oneshot = sum_theta / K                               # dlsa.py:51-52
+    if columns is None:
+        columns = [f"x{j}" for j in range(p)]
+    return pd.DataFrame(np.concatenate((beta_ols.reshape(p, 1), beta_oneshot.reshape(p, 1), S), 1),
+                        columns=["beta_byOLS", "beta_byONESHOT"] + list(columns))
+
+
+def reduce_partitions_device(fit):
+    """[sum Sig_inv | sum Sig_inv theta | sum theta | K] of a BatchedFit, as a
+    device tensor of P*P + 2P + 1 fp64 (the buffer the RCCL all-reduce sums)."""
+    import torch
+
+    P, K = fit.P, fit.K
+    out = torch.empty((P * P + 2 * P + 1,), dtype=torch.float64, device=fit.theta.device)
+    lib = _hip.load()
+    stream = ctypes.c_void_p(torch.cuda.current_stream(fit.theta.device).cuda_stream)
+    rc = lib.dlsa_reduce_partitions(ctypes.c_void_p(fit.sig_inv.data_ptr()),
+                                    ctypes.c_void_p(fit.sig_inv_theta.data_ptr()),
+                                    ctypes.c_void_p(fit.theta.data_ptr()), K, P,
+                                    ctypes.c_void_p(out.data_ptr()), stream)
+    _hip.check(rc, "dlsa_reduce_partitions")
+    return out
+
+
+def split_reduced(buf, P):
+    """Split a reduced buffer (host array) into (S, v, sum_theta, K)."""
+    b = np.asarray(buf, dtype=np.float64)
+    S = b[:P * P].reshape(P, P)
+    v = b[P * P:P * P + P]
+    st = b[P * P + P:P * P + 2 * P]
+    return S, v, st, float(b[P * P + 2 * P])
+
+
+def dlsa_mapred(model_mapped_sdf, columns=None, num_partitions=None):
+    """MapReduce combine for partitioned fits (dlsa/dlsa.py:21).
+
+    Accepts a ``BatchedFit`` (GPU), a stacked pandas frame shaped like the
+    Spark map output (``par_id, coef, Sig_invMcoef, <cols>``), or a list of
+    per-partition frames.  Returns the reference frame
+    ``[beta_byOLS, beta_byONESHOT, <sum Sig_inv columns>]``.
+    """
+    import pandas as pd
+
+    from .models import BatchedFit
+
+    if isinstance(model_mapped_sdf, BatchedFit):
+        buf = reduce_partitions_device(model_mapped_sdf).cpu().numpy()
+        S, v, st, K = split_reduced(buf, model_mapped_sdf.P)
+        if columns is None:
+            p = model_mapped_sdf.P - (1 if model_mapped_sdf.fit_intercept else 0)
+            columns = (["intercept"] if model_mapped_sdf.fit_intercept else []) + \
+                [f"x{j}" for j in range(p)]
+        return _frame(S, v, st, num_partitions or K, columns)
+    if isinstance(model_mapped_sdf, (list, tuple)):
+        model_mapped_sdf = pd.concat(list(model_mapped_sdf), axis=0, ignore_index=True)
+    df = model_mapped_sdf
+    grouped = df.groupby("par_id").sum().sort_index()          # dlsa.py:30-34
+    if grouped.shape[0] == 0:
+        raise Exception("Zero-length grouped pandas DataFrame obtained, check the input.")
+    p = grouped.shape[0]
+    K = num_partitions if num_partitions is not None else len(df) // p
+    S = grouped.iloc[:, 2:].to_numpy(dtype=np.float64)
+    v = grouped["Sig_invMcoef"].to_numpy(dtype=np.float64)
+    st = grouped["coef"].to_numpy(dtype=np.float64)
+    return _frame(S, v, st, K, list(df.columns[3:]) if columns is None else columns)
+
+
+def dlsa(Sig_inv_, beta_, sample_size, fit_intercept=False, type="lasso"):
+    """Distributed Least Squares Approximation selection step (dlsa/dlsa.py:70).
+
+    Runs the LSA path on (Sig_inv_, beta_) and returns the frame
+    ``{beta_byAIC, beta_byBIC}`` (BIC here is the paper's DBIC with
+    n = sample_size).  With ``fit_intercept`` the intercept (entry 0) is
+    restored as ``beta0 + beta_[0]`` (dlsa.py:88-95).  ``type`` defaults to
+    "lasso", the first choice of the R ``lars.lsa`` signature the reference
+    calls without a type argument (dlsa.py:77-80).
+    """
+    import pandas as pd
+
+    from .lsa import lars_lsa
+
+    b = np.asarray(beta_, dtype=np.float64).reshape(-1)
+    fit = lars_lsa(np.asarray(Sig_inv_, dtype=np.float64), b, intercept=fit_intercept,
+                   n=sample_size, type=type)
+    ia = int(np.argmin(fit["AIC"]))
+    ib = int(np.argmin(fit["BIC"]))
+    beta = fit["beta"]
+    if fit_intercept:
+        beta0 = fit["beta0"] + b[0]
+        b_aic = np.hstack([beta0[ia], beta[ia, :]])
+        b_bic = np.hstack([beta0[ib], beta[ib, :]])
+    else:
+        b_aic = beta[ia, :]
+        b_bic = beta[ib, :]
+    return pd.DataFrame({"beta_byAIC": b_aic, "beta_byBIC": b_bic})

@@ -1,0 +1,305 @@
+"""Map stage of DLSA on MI355X: per-partition logistic fits.
+
+Drop-in for dlsa/models.py of the reference (Vicky-Lamperouge/dlsa):
+
+* ``simulate_logistic``      -- models.py:6-40 (same legacy-RNG stream);
+* ``logistic_model``         -- models.py:42-147, same signature and output
+  frame; the fit itself runs on the GPU through ``logistic_model_batched``;
+* ``logistic_model_batched`` -- K partitions in one batched Newton/IRLS run
+  (the Spark ``groupby("partition_id").apply(udf)`` of
+  projects/logistic_dlsa.py:314-325, without Spark);
+* ``simulate_logistic_device`` -- synthetic data generated directly in HBM.
+
+There is no CPU implementation of the fit: without libdlsa_hip.so or a GPU
+these functions raise ``DlsaHipError``.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import warnings
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _hip
+from ._hip import DlsaHipError
+
+try:  # torch is the HBM allocator / stream provider only
+    import torch
+except ImportError:  # pragma: no cover
+    torch = None
+
+
+# ---------------------------------------------------------------------------
+# device helpers
+# ---------------------------------------------------------------------------
+
+
+def _require_gpu(device=None):
+    if torch is None or not torch.cuda.is_available():
+        raise DlsaHipError(
+            "no ROCm GPU visible: the DLSA map stage runs only as HIP kernels on "
+            "MI355X; there is no CPU fallback")
+    _hip.load()
+    return torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+
+
+def _stream(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _dev_f64(a, device):
+    if isinstance(a, torch.Tensor):
+        t = a.to(device=device, dtype=torch.float64)
+    else:
+        t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).to(device)
+    return t.contiguous()
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+# ---------------------------------------------------------------------------
+# synthetic data
+# ---------------------------------------------------------------------------
+
+
+def simulate_logistic(sample_size, p, partition_method, partition_num):
+    """Simulate data based on the logistic model (dlsa/models.py:6-40).
+
+    Same draws as the reference for the same ``np.random.seed``: ``rand(n, p)``
+    then one Bernoulli draw per row in row order (the reference's per-row
+    ``binomial(n=1, p=prob[i], size=1)`` loop, models.py:28-30, consumes the
+    legacy stream exactly like one vectorised call).  Unlike the reference the
+    frame is built once (the reference rebuilds it inside the row loop,
+    models.py:37-38, which is O(n^2)).
+    """
+    import pandas as pd
+
+    if partition_method != "systematic":
+        raise Exception("No such partition method implemented!")
+    n = int(sample_size)
+    n_true = int(p * 0.4)
+    coef_true = np.zeros((p, 1))
+    coef_true[:n_true] = 1.0
+    feats = np.random.rand(n, p) - 0.5
+    prob = 1 / (1 + np.exp(-feats.dot(coef_true)))
+    label = np.random.binomial(1, prob[:, 0])
+    pid = np.arange(n) % partition_num
+    data = np.column_stack([pid.astype(np.float64), label.astype(np.float64), feats])
+    return pd.DataFrame(data, columns=["partition_id", "label"] + [f"x{i}" for i in range(p)])
+
+
+def simulate_logistic_device(n, p, seed=2019, row0=0, device=None):
+    """Synthetic logistic data written straight into HBM:
+    X[i, j] ~ U(-1/2, 1/2), beta* = 1 on the first floor(0.4 p) columns,
+    y ~ Bernoulli(sigmoid(X beta*)), from counter-based streams (seed, row0 +
+    i).  Returns (X [n, p] fp64, y [n] fp64) on ``device``."""
+    dev = _require_gpu(device)
+    X = torch.empty((int(n), int(p)), dtype=torch.float64, device=dev)
+    y = torch.empty((int(n),), dtype=torch.float64, device=dev)
+    lib = _hip.load()
+    _hip.check(lib.dlsa_simulate_logistic(_ptr(X), _ptr(y), int(n), int(p), int(seed) & (2**64 - 1),
+                                          int(row0), _stream(dev)), "dlsa_simulate_logistic")
+    return X, y
+
+
+def partition_offsets(partition_id, num_partitions=None):
+    """Group rows by partition id: returns (order, offsets) so that rows
+    ``order[offsets[k]:offsets[k+1]]`` are partition k in their original order
+    (what Spark's repartition + groupby hand to each UDF call,
+    projects/logistic_dlsa.py:303-325)."""
+    pid = np.asarray(partition_id).astype(np.int64)
+    K = int(num_partitions) if num_partitions is not None else (int(pid.max()) + 1 if pid.size else 0)
+    order = np.argsort(pid, kind="stable")
+    offsets = np.zeros(K + 1, dtype=np.int64)
+    np.cumsum(np.bincount(pid, minlength=K), out=offsets[1:])
+    return order, offsets
+
+
+# ---------------------------------------------------------------------------
+# batched fit (the hot path)
+# ---------------------------------------------------------------------------
+
+
+@dataclass
+class BatchedFit:
+    """Result of one batched fit; tensors live in HBM."""
+    theta: "torch.Tensor"          # [K, P]  coef (intercept first)
+    sig_inv: "torch.Tensor"        # [K, P, P] X^T W X at theta
+    sig_inv_theta: "torch.Tensor"  # [K, P]  Sig_inv @ theta
+    loglik: "torch.Tensor"         # [K]
+    iters: "torch.Tensor"          # [K] int32
+    status: "torch.Tensor"         # [K] int32 (0 ok, 1 maxiter, 2 singular, 3 empty, 4 nonfinite)
+    offsets: np.ndarray            # [K+1] host
+    fit_intercept: bool
+    stats: dict = field(default_factory=dict)
+
+    @property
+    def K(self):
+        return int(self.theta.shape[0])
+
+    @property
+    def P(self):
+        return int(self.theta.shape[1])
+
+    @property
+    def n_rows(self):
+        return int(self.offsets[-1])
+
+    def status_counts(self):
+        s = self.status.cpu().numpy()
+        return {_hip.STATUS_NAMES.get(int(v), str(v)): int((s == v).sum()) for v in np.unique(s)}
+
+
+def logistic_model_batched(X, y, offsets, fit_intercept=False, center=None, scale=None,
+                           max_iter=100, tol=1e-10, hessian="mixed", switch_tol=1e-6,
+                           record_timing=False, rows_per_chunk=0, workspace=None,
+                           device=None):
+    """Fit K row partitions at once on the GPU (batched Newton/IRLS).
+
+    Per partition k (rows ``offsets[k]:offsets[k+1]`` of X) this computes what
+    ``logistic_model`` returns for one Spark group (models.py:94-131): the
+    unpenalised MLE ``theta_k`` (intercept first when ``fit_intercept``),
+    ``Sig_inv_k = X_k^T diag(p(1-p)) X_k`` at theta_k and
+    ``Sig_inv_k theta_k``.  ``center``/``scale`` standardise the columns like
+    models.py:99-101.
+
+    X: [n, p] fp64 (torch tensor on the GPU, or array-like, copied once);
+    y: [n] 0/1; offsets: K+1 host ints.  ``hessian`` = "mixed" (fp32-MFMA
+    Hessian until the Newton step is below ``switch_tol``, then an fp64-MFMA
+    pass; the gradient and the returned Sig_inv are always fp64) or "fp64".
+    """
+    dev = _require_gpu(device)
+    Xd = _dev_f64(X, dev)
+    yd = _dev_f64(y, dev).reshape(-1)
+    if Xd.dim() != 2:
+        raise ValueError("X must be 2-D [n, p]")
+    n, p = Xd.shape
+    offs = np.ascontiguousarray(np.asarray(offsets, dtype=np.int64))
+    K = offs.size - 1
+    if K < 1 or offs[0] != 0 or offs[-1] != n or np.any(np.diff(offs) < 0):
+        raise ValueError("offsets must be non-decreasing, start at 0 and end at n")
+    if yd.numel() != n:
+        raise ValueError("y must have n entries")
+    P = p + (1 if fit_intercept else 0)
+    if P > _hip.MAX_P_FUSED:
+        raise DlsaHipError(f"P = {P} > {_hip.MAX_P_FUSED} not supported by the fused pass yet")
+    cd = sd = None
+    if center is not None or scale is not None:
+        cd = _dev_f64(center, dev).reshape(-1)
+        sd = _dev_f64(scale, dev).reshape(-1)
+        if cd.numel() != p or sd.numel() != p:
+            raise ValueError("center/scale must have p entries")
+    theta = torch.empty((K, P), dtype=torch.float64, device=dev)
+    sig = torch.empty((K, P, P), dtype=torch.float64, device=dev)
+    sigt = torch.empty((K, P), dtype=torch.float64, device=dev)
+    ll = torch.empty((K,), dtype=torch.float64, device=dev)
+    iters = torch.empty((K,), dtype=torch.int32, device=dev)
+    status = torch.empty((K,), dtype=torch.int32, device=dev)
+
+    lib = _hip.load()
+    opt = _hip.default_options()
+    opt.hessian_mode = {"mixed": _hip.HESSIAN_MIXED, "fp64": _hip.HESSIAN_FP64}[hessian]
+    opt.switch_tol = float(switch_tol)
+    opt.record_timing = 1 if record_timing else 0
+    opt.rows_per_chunk = int(rows_per_chunk)
+    offs_p = offs.ctypes.data_as(ctypes.c_void_p)
+    need = lib.dlsa_logistic_workspace_bytes(offs_p, K, p, int(bool(fit_intercept)),
+                                             opt.rows_per_chunk)
+    if need < 0:
+        raise DlsaHipError(_hip.last_error())
+    if workspace is None or workspace.numel() < need:
+        workspace = torch.empty((max(int(need), 1),), dtype=torch.uint8, device=dev)
+    opt.workspace = workspace.data_ptr()
+    opt.workspace_bytes = workspace.numel()
+    rc = lib.dlsa_logistic_fit_batched_ex(
+        _ptr(Xd), _ptr(yd), offs_p, K, p, int(bool(fit_intercept)), _ptr(cd), _ptr(sd),
+        int(max_iter), float(tol), _ptr(theta), _ptr(sig), _ptr(sigt), _ptr(ll), _ptr(iters),
+        _ptr(status), ctypes.byref(opt), _stream(dev))
+    _hip.check(rc, "dlsa_logistic_fit_batched_ex")
+    stats = _hip.last_fit_stats()
+    stats["workspace_bytes"] = int(need)
+    return BatchedFit(theta, sig, sigt, ll, iters, status, offs, bool(fit_intercept), stats)
+
+
+# ---------------------------------------------------------------------------
+# reference-signature wrapper (one Spark group)
+# ---------------------------------------------------------------------------
+
+
+def _describe_row(data_info, col, row):
+    # Spark DataFrame.describe().toPandas(): rows count/mean/stddev/min/max,
+    # values as strings (models.py:99-101 reads rows 1 and 2)
+    return float(data_info[col][row])
+
+
+def _design(sample_df, Y_name, dummy_info, dummy_factors_baseline):
+    """Host-side design matrix of one partition, models.py:56-104.  Returns
+    (x_train DataFrame, usecols_x0 numeric columns, usecols_x all columns,
+    zero_frame_or_None)."""
+    import pandas as pd
+
+    if len(dummy_info) > 0:
+        factors = list(dummy_info["factor_selected"].keys())
+        dropped = {k: v for k, v in dummy_info["factor_dropped"].items() if len(v) > 0}
+        df = sample_df.replace(dropped, "000_OTHERS")
+        wide = pd.get_dummies(data=df, drop_first=False, columns=factors, sparse=True)
+        x_train = wide.drop(["partition_id", Y_name] + list(dummy_factors_baseline), axis=1)
+        numeric = sorted(set(df.columns.drop(["partition_id", Y_name])) - set(factors))
+        cols = list(numeric)
+        for f in factors:
+            cols.extend(sorted(dummy_info["factor_selected_names"][f]))
+        cols = [c for c in cols if c not in dummy_factors_baseline]
+        if set(x_train.columns) != set(cols):
+            return x_train, numeric, cols, True
+        return x_train, numeric, cols, False
+    x_train = sample_df.drop(["partition_id", Y_name] + list(dummy_factors_baseline), axis=1)
+    return x_train, list(x_train.columns), list(x_train.columns), False
+
+
+def logistic_model(sample_df, Y_name, fit_intercept=False, dummy_info=[], dummy_factors_baseline=[],
+                   data_info=[]):
+    """Run the logistic model on one partition (dlsa/models.py:42-147).
+
+    Same inputs and the same p x (p+3) output frame as the reference:
+    ``par_id | coef | Sig_invMcoef | <Sig_inv columns>``, intercept first.
+    A partition that lacks a selected dummy level returns the reference's
+    all-zero frame (models.py:84-91).  The estimate is the converged MLE (the
+    reference stops sklearn at its default tol=1e-4); the fit runs on the GPU.
+    """
+    import pandas as pd
+
+    icpt = ["intercept"] if fit_intercept else []
+    x_train, numeric, cols, missing = _design(sample_df, Y_name, dummy_info, dummy_factors_baseline)
+    if missing:
+        warnings.warn("Dummies:" + str(set(cols) - set(x_train.columns))
+                      + "missing in this data chunk " + str(x_train.shape)
+                      + "Skip modeling this part of data.")
+        return pd.DataFrame(0, index=np.arange(len(icpt + cols)),
+                            columns=["par_id", "coef", "Sig_invMcoef"] + icpt + cols)
+    x_train = x_train.reindex(columns=cols)
+    X = np.ascontiguousarray(x_train.to_numpy(dtype=np.float64))
+    y = np.asarray(sample_df[Y_name], dtype=np.float64)
+    center = scale = None
+    if len(data_info) > 0:
+        center = np.zeros(len(cols))
+        scale = np.ones(len(cols))
+        for j, c in enumerate(cols):
+            if c in numeric:
+                center[j] = _describe_row(data_info, c, 1)
+                scale[j] = _describe_row(data_info, c, 2)
+    fit = logistic_model_batched(X, y, np.array([0, X.shape[0]]), fit_intercept=fit_intercept,
+                                 center=center, scale=scale)
+    coef = fit.theta[0].cpu().numpy()
+    sig = fit.sig_inv[0].cpu().numpy()
+    sigt = fit.sig_inv_theta[0].cpu().numpy()
+    P = coef.size
+    out = pd.DataFrame(np.column_stack([coef, sigt, sig]),
+                       columns=pd.Index(["coef", "Sig_invMcoef"] + icpt + cols))
+    out.insert(0, "par_id", np.arange(P))
+    if out.isna().values.any():
+        warnings.warn("NAs appear in the final output")
+    return out

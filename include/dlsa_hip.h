@@ -1,0 +1,195 @@
+/*
+ * dlsa_hip.h -- C-ABI of libdlsa_hip.so, the MI355X (gfx950) DLSA estimator.
+ *
+ * This is the drop-in boundary for the reference's map/combine/select path
+ * (Vicky-Lamperouge/dlsa).  The reference has no FFI: its map stage is a
+ * Spark GROUPED_MAP pandas_udf around dlsa/models.py:logistic_model, its
+ * combine is dlsa/dlsa.py:dlsa_mapred and its selection step is
+ * dlsa/lsa.py:lars_lsa (or R lars.lsa via rpy2, dlsa/dlsa.py:64-81).  Each
+ * entry point below names the reference interface it replaces.  The Python
+ * binding (ctypes) lives in dlsa_amd/_hip.py; INTEGRATION.md shows the stub a
+ * maintainer would add on the reference side.
+ *
+ * Conventions
+ *   - Plain C types only.  Pointers named X/y/theta/... are DEVICE pointers
+ *     (hipMalloc'd or torch tensor data_ptr()), except where "host" is noted.
+ *   - The caller owns every buffer.  Scratch comes from the caller's
+ *     workspace (dlsa_fit_options.workspace) or, when that is NULL, is
+ *     hipMallocAsync'd on the stream and freed before return.
+ *   - Work is enqueued on the caller's hipStream_t (`stream`, NULL = default
+ *     stream).  dlsa_logistic_fit_batched* reads a 16-byte device counter
+ *     back once per Newton iteration (a stream synchronisation); the other
+ *     device entry points are fully asynchronous.
+ *   - Return 0 on success, a negative DLSA_E_* code on failure; the message
+ *     is in dlsa_last_error() (thread-local).
+ *   - Row-major fp64.  Partition k owns rows offsets[k] .. offsets[k+1]-1 of X
+ *     (partitions contiguous: the layout Spark's repartition(K,
+ *     "partition_id") + groupby produce per task, projects/logistic_dlsa.py:
+ *     303-325).  X must be readable up to the next 16-byte boundary past its
+ *     last element (true for any torch/hipMalloc allocation that starts at
+ *     the tensor).
+ *   - P = p + fit_intercept is the parameter count; with an intercept the
+ *     intercept is parameter 0 (dlsa/models.py:116-122).
+ */
+#ifndef DLSA_HIP_H
+#define DLSA_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* error codes */
+#define DLSA_OK 0
+#define DLSA_E_INVALID (-1)
+#define DLSA_E_HIP (-2)
+#define DLSA_E_UNSUPPORTED (-3)
+#define DLSA_E_WORKSPACE (-4)
+
+/* per-partition status (status[] output) -- SURVEY.md section 5: the
+ * reference only warns (models.py:84-91,144-145); here every partition
+ * reports what happened. */
+#define DLSA_STATUS_OK 0          /* converged */
+#define DLSA_STATUS_MAXITER 1     /* max_iter reached; last iterate returned */
+#define DLSA_STATUS_SINGULAR 2    /* X^T W X not positive definite */
+#define DLSA_STATUS_EMPTY 3       /* no rows: zero block, like models.py:84-91 */
+#define DLSA_STATUS_NONFINITE 4   /* NaN/Inf in the data or the iterates */
+
+/* Hessian arithmetic of the Newton passes */
+#define DLSA_HESSIAN_MIXED 0  /* fp32 MFMA Hessian until the step is below
+                                 switch_tol, then one fp64 MFMA pass; the
+                                 gradient, the log-likelihood and the returned
+                                 Sig_inv are always fp64 */
+#define DLSA_HESSIAN_FP64 1   /* fp64 MFMA Hessian on every pass */
+
+#define DLSA_MAX_P_FUSED 128  /* largest P handled by the per-wave fused pass */
+
+typedef struct dlsa_fit_options {
+  int32_t hessian_mode;     /* DLSA_HESSIAN_MIXED (default) or _FP64 */
+  int32_t record_timing;    /* 1: time every launch with hipEvents, see
+                               dlsa_last_fit_stats() */
+  double switch_tol;        /* MIXED: relative step size that triggers the fp64
+                               pass (<= 0: default 1e-6) */
+  void* workspace;          /* device scratch, NULL: allocate per call */
+  int64_t workspace_bytes;  /* size of `workspace` */
+  int32_t rows_per_chunk;   /* <= 0: automatic (rows one wave streams) */
+  int32_t reserved[7];
+} dlsa_fit_options;
+
+typedef struct dlsa_fit_stats {
+  int32_t iterations;       /* Newton iterations run (max over partitions) */
+  int32_t passes_fp32;      /* fp32-Hessian pass launches */
+  int32_t passes_fp64;      /* fp64-Hessian pass launches */
+  int32_t n_chunks;         /* waves per pass launch */
+  double ms_pass_fp32;      /* summed kernel time (record_timing only) */
+  double ms_pass_fp64;
+  double ms_solve;          /* per-partition Cholesky/Newton update kernels */
+  double ms_total;          /* whole call, host wall clock */
+  int64_t rows_fp32;        /* rows streamed by fp32 passes (sum) */
+  int64_t rows_fp64;        /* rows streamed by fp64 passes (sum) */
+} dlsa_fit_stats;
+
+/* Default options (mixed Hessian, automatic chunking, no timing). */
+void dlsa_fit_options_default(dlsa_fit_options* opt);
+
+/* Device scratch needed by a fit with these partitions (offsets: HOST array of
+ * K+1 int64).  Pass at least this many bytes in dlsa_fit_options.workspace. */
+int64_t dlsa_logistic_workspace_bytes(const int64_t* offsets, int32_t K,
+                                      int32_t p, int32_t fit_intercept,
+                                      int32_t rows_per_chunk);
+
+/*
+ * Batched local logistic fit -- replaces the body of the map-stage UDF,
+ * dlsa/models.py:42-147 logistic_model(), for K partitions at once:
+ *   standardise (models.py:99-101; center/scale may be NULL),
+ *   unpenalised logistic MLE (sklearn newton-cg, models.py:110-113),
+ *   theta = [b0, b] with the intercept first (models.py:116-122),
+ *   Sig_inv = X^T diag(p(1-p)) X at theta (models.py:130),
+ *   Sig_invMcoef = Sig_inv theta (models.py:131).
+ * Newton/IRLS from theta = 0; converged when max|step| <= tol*(1+max|theta|).
+ *
+ *  X        [n_total, p] fp64 row-major, device
+ *  y        [n_total] fp64 0/1 labels, device
+ *  offsets  [K+1] int64, HOST, offsets[0] = 0, non-decreasing
+ *  center, scale  [p] fp64 device or NULL (both or neither)
+ *  theta          [K, P] out     sig_inv       [K, P, P] out
+ *  sig_inv_theta  [K, P] out     loglik        [K] out (at theta)
+ *  iters          [K] int32 out  status        [K] int32 out (DLSA_STATUS_*)
+ * 1 <= P <= DLSA_MAX_P_FUSED.
+ */
+int dlsa_logistic_fit_batched(const double* X, const double* y,
+                              const int64_t* offsets, int32_t K, int32_t p,
+                              int32_t fit_intercept, const double* center,
+                              const double* scale, int32_t max_iter,
+                              double tol, double* theta, double* sig_inv,
+                              double* sig_inv_theta, double* loglik,
+                              int32_t* iters, int32_t* status, void* stream);
+
+/* Same, with options (Hessian mode, caller workspace, timing). */
+int dlsa_logistic_fit_batched_ex(const double* X, const double* y,
+                                 const int64_t* offsets, int32_t K, int32_t p,
+                                 int32_t fit_intercept, const double* center,
+                                 const double* scale, int32_t max_iter,
+                                 double tol, double* theta, double* sig_inv,
+                                 double* sig_inv_theta, double* loglik,
+                                 int32_t* iters, int32_t* status,
+                                 const dlsa_fit_options* opt, void* stream);
+
+/* Timing/iteration record of the calling thread's last fit. */
+int dlsa_last_fit_stats(dlsa_fit_stats* out);
+
+/*
+ * Local pre-reduction of this device's partitions -- the group-sum of
+ * dlsa/dlsa.py:30-34 (groupby('par_id').sum), done in HBM before the one
+ * RCCL all-reduce that replaces the Spark shuffle + collect:
+ *   out[0 : P*P]          = sum_k sig_inv[k]
+ *   out[P*P : P*P+P]      = sum_k sig_inv_theta[k]
+ *   out[P*P+P : P*P+2P]   = sum_k theta[k]
+ *   out[P*P+2P]           = K   (partition count, for ONESHOT, dlsa.py:51-52)
+ * Deterministic (fixed summation order over k).
+ */
+int dlsa_reduce_partitions(const double* sig_inv, const double* sig_inv_theta,
+                           const double* theta, int32_t K, int32_t p,
+                           double* out, void* stream);
+
+/*
+ * Synthetic logistic data in HBM (the input generator of SURVEY 8(d) for
+ * configs too large for the host): X[i, j] = u(seed, row0 + i, j) - 0.5 with
+ * u a counter-based (splitmix64) U[0,1) double; beta* = 1 on the first
+ * floor(0.4 p) columns (dlsa/models.py:12-19); y ~ Bernoulli(sigmoid(X beta*))
+ * drawn from an independent counter stream (models.py:23-30).  Rows are
+ * written partition-contiguous; row0 offsets the counter so shards on
+ * different GPUs draw disjoint rows.  Bit-exact with the numpy restatement
+ * in oracle/ (simulate_counter).
+ */
+int dlsa_simulate_logistic(double* X, double* y, int64_t n, int32_t p,
+                           uint64_t seed, int64_t row0, void* stream);
+
+/*
+ * LARS / adaptive-lasso path on the LSA quadratic form, HOST code --
+ * replaces dlsa/lsa.py:90-212 lars_lsa (and R lars.lsa called from
+ * dlsa/dlsa.py:77-80).  Sigma0 [P*P] row-major and b0 [P] are HOST arrays.
+ * type: 0 = "lar", 1 = "lasso".  max_steps <= 0 means 8*m (lsa.py:116-117)
+ * with m = P - intercept.  Outputs (HOST, caller-allocated for
+ * max_steps+1 rows): beta [(max_steps+1) * m] row-major, beta0, aic, bic
+ * [max_steps+1]; *n_steps = number of rows written (k+1).
+ * Reference defects fixed: lsa.py:100 (intercept indexes range(1, n) with the
+ * sample size), lsa.py:141-142 (singular back-out).
+ */
+int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
+                  int32_t intercept, double n, int32_t type, double eps,
+                  int32_t max_steps, double* beta, double* beta0, double* aic,
+                  double* bic, int32_t* n_steps);
+
+/* Thread-local message of the last failing call ("" if none). */
+const char* dlsa_last_error(void);
+
+/* Library build identification (gfx target, git-independent version). */
+const char* dlsa_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DLSA_HIP_H */

@@ -19,6 +19,7 @@ the agreement).  See DESIGN.md section "Oracle".
 from .dlsa_oracle import (  # noqa: F401
     simulate_logistic_arrays,
     simulate_logistic,
+    simulate_counter,
     systematic_partition,
     logistic_fit,
     logistic_fit_partitions,

@@ -60,6 +60,40 @@ def simulate_logistic(sample_size, p, partition_method="systematic",
                         ["x" + str(x) for x in range(p)])
 
 
+_M64 = (1 << 64) - 1
+_Y_SALT = 0x5DEECE66D
+
+
+def _u01_counter(seed, ctr):
+    """splitmix64 finaliser of (seed + (ctr+1) * golden) -> U[0,1) with 53 bits
+    (dlsa_amd/csrc/aux_kernels.hip:u01), vectorised over uint64 counters."""
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed & _M64) + (ctr.astype(np.uint64) + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return (z >> np.uint64(11)).astype(np.float64) * (2.0 ** -53)
+
+
+def simulate_counter(n, p, seed=2019, row0=0):
+    """Host restatement of the device generator ``dlsa_simulate_logistic``
+    (SURVEY 8(d) large-config input): same distribution as
+    ``simulate_logistic`` (X ~ U(-1/2, 1/2), beta* = 1 on the first
+    floor(0.4 p) columns, y ~ Bernoulli(sigmoid(X beta*))) from counter-based
+    streams, so the GPU can generate 80 GB in place and the host can
+    regenerate any rows bit for bit."""
+    rows = np.arange(row0, row0 + n, dtype=np.uint64)
+    ctr = rows[:, None] * np.uint64(p) + np.arange(p, dtype=np.uint64)[None, :]
+    X = _u01_counter(seed, ctr) - 0.5
+    p1 = int(p * 0.4)
+    eta = np.zeros(n)
+    for j in range(p1):  # sequential order, as the device loop
+        eta = eta + X[:, j]
+    prob = 1.0 / (1.0 + np.exp(-eta))
+    y = (_u01_counter(seed ^ _Y_SALT, rows) < prob).astype(np.float64)
+    return X, y
+
+
 def systematic_partition(partition_id):
     """Stable grouping of rows by partition id (Spark ``groupby`` at
     projects/logistic_dlsa.py:325 hands each group to the UDF in row order).

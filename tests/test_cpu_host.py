@@ -1,0 +1,199 @@
+"""CPU tests of the product's host side: the C-ABI library loads and exports
+every declared symbol, the native LARS/DBIC and the combine match the
+reference golden vectors and the oracle, the product fails loudly without a
+GPU, and the multi-rank combine is correct under gloo (world_size 2)."""
+
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_symbols():
+    txt = open(os.path.join(ROOT, "include", "dlsa_hip.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(dlsa_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    import ctypes
+
+    from dlsa_amd import _hip
+
+    lib = ctypes.CDLL(_hip.LIB_PATH)
+    syms = _header_symbols()
+    assert len(syms) >= 10
+    for s in syms:
+        assert hasattr(lib, s), f"{s} declared in include/dlsa_hip.h but not exported"
+    assert set(syms) == set(_hip.SIGNATURES), "ctypes binding out of sync with the header"
+    assert b"gfx950" in _hip.load().dlsa_build_info()
+
+
+def test_fit_fails_loudly_without_gpu():
+    import torch
+
+    from dlsa_amd import DlsaHipError
+    from dlsa_amd.models import logistic_model_batched
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(DlsaHipError):
+        logistic_model_batched(np.zeros((4, 2)), np.zeros(4), [0, 4])
+
+
+@pytest.mark.parametrize("typ", ["lar", "lasso"])
+def test_native_lars_config1_golden(golden_dir, typ):
+    from dlsa_amd.lsa import lars_lsa
+
+    g = np.load(os.path.join(golden_dir, "config1_n1e5_p10_K4.npz"))
+    S = g["outs_noint"][:, :, 3:].sum(0)
+    r = lars_lsa(S, g["wlse_noint"], False, 100000, type=typ)
+    assert r["beta"].shape == g[f"lars_{typ}_beta"].shape
+    assert np.abs(r["beta"] - g[f"lars_{typ}_beta"]).max() < 1e-12
+    assert np.abs(r["BIC"] - g[f"lars_{typ}_BIC"]).max() < 1e-8
+    assert np.abs(r["AIC"] - g[f"lars_{typ}_AIC"]).max() < 1e-8
+
+
+def test_native_lars_drop_cases_golden(golden_dir):
+    from dlsa_amd.lsa import lars_lsa
+
+    L = np.load(os.path.join(golden_dir, "lars_cases.npz"))
+    for i in range(int(L["ncases"])):
+        for typ in ("lar", "lasso"):
+            r = lars_lsa(L[f"c{i}_S"], L[f"c{i}_b"], False, 500, type=typ)
+            gb = L[f"c{i}_{typ}_beta"]
+            assert r["beta"].shape == gb.shape
+            assert np.abs(r["beta"] - gb).max() < 1e-10
+            assert np.abs(r["BIC"] - L[f"c{i}_{typ}_BIC"]).max() < 1e-8
+
+
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("intercept", [False, True])
+@pytest.mark.parametrize("typ", ["lar", "lasso"])
+def test_native_lars_vs_oracle_random(seed, intercept, typ):
+    from dlsa_amd.lsa import lars_lsa
+
+    rs = np.random.RandomState(seed)
+    m = [5, 12, 30, 60, 3, 101][seed]
+    A = rs.randn(2 * m + 5, m)
+    A[:, 1 % m] += 0.8 * A[:, 0]
+    S = A.T @ A
+    b = rs.randn(m) * (rs.rand(m) < 0.5) + 0.05 * rs.randn(m)
+    r = lars_lsa(S, b, intercept, 1000, type=typ)
+    o = O.lars_lsa(S, b, intercept, 1000, type=typ)
+    assert r["beta"].shape == o["beta"].shape
+    assert np.allclose(r["beta"], o["beta"], rtol=0, atol=1e-9 * max(1, np.abs(o["beta"]).max()))
+    assert np.allclose(r["BIC"], o["BIC"], rtol=1e-10, atol=1e-8)
+    assert np.allclose(r["beta0"], o["beta0"], rtol=1e-10, atol=1e-10)
+
+
+@pytest.mark.parametrize("fi", [False, True])
+def test_dlsa_selection_vs_oracle(golden_dir, fi):
+    from dlsa_amd.dlsa import dlsa
+
+    g = np.load(os.path.join(golden_dir, "config1_n1e5_p10_K4.npz"))
+    tag = "int" if fi else "noint"
+    S = g["outs_" + tag][:, :, 3:].sum(0)
+    w = g["wlse_" + tag]
+    out = dlsa(S, w, 100000, fit_intercept=fi)
+    oa, ob = O.dlsa(S, w, 100000, fit_intercept=fi)
+    assert np.allclose(out["beta_byAIC"], oa, atol=1e-12)
+    assert np.allclose(out["beta_byBIC"], ob, atol=1e-12)
+    # DBIC picks the true support {x0..x3}
+    sup = np.nonzero(out["beta_byBIC"].to_numpy()[1 if fi else 0:])[0]
+    assert set(sup) == {0, 1, 2, 3}
+
+
+def test_dlsa_mapred_pandas_vs_golden(golden_dir):
+    """Stacked Spark-style map output (par_id, coef, Sig_invMcoef, cols)."""
+    import pandas as pd
+
+    from dlsa_amd.dlsa import dlsa_mapred
+
+    g = np.load(os.path.join(golden_dir, "config1_n1e5_p10_K4.npz"))
+    outs = g["outs_int"]
+    cols = ["par_id", "coef", "Sig_invMcoef", "intercept"] + [f"x{i}" for i in range(10)]
+    frames = [pd.DataFrame(o, columns=cols) for o in outs]
+    res = dlsa_mapred(frames)
+    assert list(res.columns[:2]) == ["beta_byOLS", "beta_byONESHOT"]
+    assert np.abs(res["beta_byOLS"].to_numpy() - g["wlse_int"]).max() < 1e-12
+    assert np.abs(res["beta_byONESHOT"].to_numpy() - g["oneshot_int"]).max() < 1e-12
+    assert np.allclose(res.iloc[:, 2:].to_numpy(), outs[:, :, 3:].sum(0), rtol=1e-13, atol=1e-12)
+    with pytest.raises(Exception):
+        dlsa_mapred(pd.DataFrame(columns=cols))
+
+
+@pytest.mark.parametrize("name", ["simulate_s2019_n3000_p10_K4.npz", "simulate_s7_n600_p7_K3.npz"])
+def test_simulate_logistic_product_bit_identical(golden_dir, name):
+    from dlsa_amd.models import simulate_logistic
+
+    g = np.load(os.path.join(golden_dir, name))
+    np.random.seed(int(g["seed"]))
+    df = simulate_logistic(int(g["n"]), int(g["p"]), "systematic", int(g["K"]))
+    assert np.array_equal(df.to_numpy(np.float64), g["data"])
+
+
+def test_partition_offsets():
+    from dlsa_amd.models import partition_offsets
+
+    pid = np.arange(23) % 5
+    order, off = partition_offsets(pid)
+    assert off.tolist() == [0, 5, 10, 15, 19, 23]
+    assert all((pid[order[off[k]:off[k + 1]]] == k).all() for k in range(5))
+    assert all(np.all(np.diff(order[off[k]:off[k + 1]]) > 0) for k in range(5))
+
+
+# ---- multi-rank combine (gloo, world_size 2) -------------------------------
+
+def _gloo_worker(rank, world, port, golden_dir, q):
+    import torch
+    import torch.distributed as dist
+
+    from dlsa_amd.distributed import combine, finish
+    from dlsa_amd.dlsa import split_reduced
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = np.load(os.path.join(golden_dir, "config1_n1e5_p10_K4.npz"))
+    outs = g["outs_noint"]
+    mine = outs[rank::world]  # partitions sharded over ranks
+    P = outs.shape[1]
+    buf = np.concatenate([mine[:, :, 3:].sum(0).ravel(), mine[:, :, 2].sum(0),
+                          mine[:, :, 1].sum(0), [float(len(mine))]])
+    t = torch.from_numpy(buf)
+    combine(t)
+    S, v, st, K = split_reduced(t.numpy(), P)
+    res = finish(S, v, st, K, 100000)
+    q.put((rank, res["wlse"], res["oneshot"], res["dbic_support"].tolist(), K))
+    dist.destroy_process_group()
+
+
+def test_distributed_combine_gloo(golden_dir):
+    import multiprocessing as mp
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_gloo_worker, args=(r, 2, port, golden_dir, q)) for r in range(2)]
+    for p_ in ps:
+        p_.start()
+    res = [q.get(timeout=120) for _ in range(2)]
+    for p_ in ps:
+        p_.join(timeout=60)
+        assert p_.exitcode == 0
+    g = np.load(os.path.join(golden_dir, "config1_n1e5_p10_K4.npz"))
+    for rank, wlse, oneshot, support, K in res:
+        assert K == 4
+        assert np.abs(wlse - g["wlse_noint"]).max() < 1e-10
+        assert np.abs(oneshot - g["oneshot_noint"]).max() < 1e-12
+        assert support == [0, 1, 2, 3]

@@ -1,0 +1,232 @@
+"""GPU parity: the HIP path (libdlsa_hip.so through its C-ABI) against the
+reference golden vectors and the pinned CPU oracle.
+
+Tolerance contract (BASELINE.json north_star): theta_k, Sig_inv_k and the
+combined estimate within 1e-8 relative (fp64); identical DBIC-selected
+support.  Integer/index outputs (status, counts, generator bits) exact.
+"""
+
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+REL = 1e-8  # north_star tolerance, relative to the largest entry
+
+
+def _rel(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return np.abs(a - b).max() / max(np.abs(b).max(), 1e-300)
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need a visible MI355X"
+    return torch
+
+
+@pytest.fixture(scope="module")
+def M():
+    from dlsa_amd import models
+    return models
+
+
+def _golden(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name))
+
+
+def _config1(golden_dir):
+    g = _golden(golden_dir, "config1_n1e5_p10_K4.npz")
+    np.random.seed(int(g["seed"]))
+    pid, lab, feat = O.simulate_logistic_arrays(100000, 10, "systematic", 4)
+    order, off = O.systematic_partition(pid)
+    return g, feat[order], lab[order], off
+
+
+@pytest.mark.parametrize("hessian", ["mixed", "fp64"])
+@pytest.mark.parametrize("tag,fi", [("noint", False), ("int", True)])
+def test_config1_vs_reference(golden_dir, torch_cuda, M, hessian, tag, fi):
+    from dlsa_amd.dlsa import dlsa, dlsa_mapred
+
+    g, X, y, off = _config1(golden_dir)
+    fit = M.logistic_model_batched(X, y, off, fit_intercept=fi, hessian=hessian)
+    outs = g["outs_" + tag]
+    assert fit.status.cpu().numpy().tolist() == [0, 0, 0, 0]
+    assert _rel(fit.theta.cpu(), outs[:, :, 1]) < REL
+    assert _rel(fit.sig_inv.cpu(), outs[:, :, 3:]) < REL
+    assert _rel(fit.sig_inv_theta.cpu(), outs[:, :, 2]) < REL
+    comb = dlsa_mapred(fit)
+    assert _rel(comb["beta_byOLS"], g["wlse_" + tag]) < REL
+    assert _rel(comb["beta_byONESHOT"], g["oneshot_" + tag]) < REL
+    if not fi:
+        sel = dlsa(comb.iloc[:, 2:], comb["beta_byOLS"], 100000, fit_intercept=False, type="lasso")
+        gb = g["lars_lasso_beta"][int(np.argmin(g["lars_lasso_BIC"]))]
+        assert set(np.nonzero(sel["beta_byBIC"].to_numpy())[0]) == set(np.nonzero(gb)[0])
+
+
+def test_p100_vs_reference(golden_dir, torch_cuda, M):
+    from dlsa_amd.dlsa import dlsa, dlsa_mapred
+
+    P = _golden(golden_dir, "p100_n8e4_K4.npz")
+    np.random.seed(int(P["seed"]))
+    pid, lab, feat = O.simulate_logistic_arrays(80000, 100, "systematic", 4)
+    order, off = O.systematic_partition(pid)
+    fit = M.logistic_model_batched(feat[order], lab[order], off)
+    assert (fit.status.cpu().numpy() == 0).all()
+    assert _rel(fit.theta.cpu(), P["outs"][:, :, 1]) < REL
+    assert _rel(fit.sig_inv.cpu(), P["outs"][:, :, 3:]) < REL
+    comb = dlsa_mapred(fit)
+    assert _rel(comb["beta_byOLS"], P["wlse"]) < REL
+    sel = dlsa(comb.iloc[:, 2:], comb["beta_byOLS"], 80000, type="lasso")
+    gb = P["lars_lasso_beta"][int(np.argmin(P["lars_lasso_BIC"]))]
+    assert set(np.nonzero(sel["beta_byBIC"].to_numpy())[0]) == set(np.nonzero(gb)[0])
+
+
+def test_games_expand_vs_reference(golden_dir, torch_cuda, M):
+    G = _golden(golden_dir, "games_expand.npz")
+    X, y = G["X"].astype(float), G["y"].astype(float)
+    order, off = O.systematic_partition(np.arange(len(y)) % 2)
+    fit = M.logistic_model_batched(X[order], y[order], off)
+    assert _rel(fit.theta.cpu(), G["outs"][:, :, 1]) < REL
+    assert _rel(fit.sig_inv.cpu(), G["outs"][:, :, 3:]) < REL
+
+
+def test_standardized_intercept_vs_reference(golden_dir, torch_cuda, M):
+    D = _golden(golden_dir, "standardized_intercept.npz")
+    order, off = O.systematic_partition(np.arange(len(D["y"])) % 3)
+    fit = M.logistic_model_batched(D["X"][order], D["y"][order], off, fit_intercept=True,
+                                   center=D["center"], scale=D["scale"])
+    assert _rel(fit.theta.cpu(), D["outs"][:, :, 1]) < REL
+    assert _rel(fit.sig_inv.cpu(), D["outs"][:, :, 3:]) < REL
+
+
+def test_logistic_model_reference_signature(golden_dir, torch_cuda, M):
+    """models.py:42 signature and p x (p+3) frame, one Spark group."""
+    import pandas as pd
+
+    g, X, y, off = _config1(golden_dir)
+    k = 2
+    df = pd.DataFrame(np.column_stack([np.full(off[k + 1] - off[k], k), y[off[k]:off[k + 1]],
+                                       X[off[k]:off[k + 1]]]),
+                      columns=["partition_id", "label"] + [f"x{i}" for i in range(10)])
+    out = M.logistic_model(df, "label", fit_intercept=True)
+    assert list(out.columns) == ["par_id", "coef", "Sig_invMcoef", "intercept"] + \
+        [f"x{i}" for i in range(10)]
+    assert _rel(out.to_numpy(), g["outs_int"][k]) < REL
+
+
+def test_device_generator_matches_host(torch_cuda, M):
+    X, y = M.simulate_logistic_device(5000, 37, seed=123, row0=777)
+    Xh, yh = O.simulate_counter(5000, 37, seed=123, row0=777)
+    assert np.array_equal(X.cpu().numpy(), Xh)
+    assert np.array_equal(y.cpu().numpy(), yh)
+
+
+@pytest.mark.parametrize("p,fi", [(1, False), (1, True), (15, True), (16, False), (16, True),
+                                  (33, False), (64, True), (100, False), (127, True), (128, False)])
+def test_shapes_vs_oracle(torch_cuda, M, p, fi):
+    """Every column-tile count NT = 1..8 and the partial-tile / intercept
+    edges, ragged partition sizes (incl. one < 8 rows block tail)."""
+    sizes = [3001, 1500, 4096, 2003]
+    n = sum(sizes)
+    X, y = O.simulate_counter(n, p, seed=p * 7 + fi)
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    fit = M.logistic_model_batched(X, y, off, fit_intercept=fi, rows_per_chunk=1000)
+    th, S, St, ll, it = O.logistic_fit_partitions(X, y, off, fit_intercept=fi)
+    assert (fit.status.cpu().numpy() == 0).all()
+    assert _rel(fit.theta.cpu(), th) < REL
+    assert _rel(fit.sig_inv.cpu(), S) < REL
+    assert _rel(fit.sig_inv_theta.cpu(), St) < REL
+    assert _rel(fit.loglik.cpu(), ll) < 1e-10
+
+
+def test_misaligned_x_view(torch_cuda, M):
+    """X starting 8 bytes off a 16-byte boundary (LDS-DMA shift path)."""
+    torch = torch_cuda
+    n, p = 5000, 7
+    X, y = O.simulate_counter(n, p, seed=5)
+    big = torch.zeros((n * p + 1,), dtype=torch.float64, device="cuda")
+    big[1:] = torch.from_numpy(X.reshape(-1)).cuda()
+    Xv = big[1:].view(n, p)
+    assert Xv.data_ptr() % 16 == 8
+    off = np.array([0, 2500, n])
+    fit = M.logistic_model_batched(Xv, y, off, rows_per_chunk=700)
+    th, S, _, _, _ = O.logistic_fit_partitions(X, y, off)
+    assert _rel(fit.theta.cpu(), th) < REL
+    assert _rel(fit.sig_inv.cpu(), S) < REL
+
+
+def test_edge_partitions(torch_cuda, M):
+    """Empty partition -> zero block (models.py:84-91 semantics), tiny
+    partitions -> non-ok status without disturbing the others."""
+    p = 5
+    sizes = [2000, 0, 3, 2500]
+    n = sum(sizes)
+    X, y = O.simulate_counter(n, p, seed=9)
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    fit = M.logistic_model_batched(X, y, off, max_iter=30)
+    st = fit.status.cpu().numpy()
+    assert st[1] == 3  # empty
+    assert np.all(fit.sig_inv[1].cpu().numpy() == 0) and np.all(fit.theta[1].cpu().numpy() == 0)
+    assert st[2] != 0  # 3 rows, 5 parameters: singular / no MLE
+    for k in (0, 3):
+        o = O.logistic_fit(X[off[k]:off[k + 1]], y[off[k]:off[k + 1]])
+        assert st[k] == 0
+        assert _rel(fit.theta[k].cpu(), o["coef"]) < REL
+        assert _rel(fit.sig_inv[k].cpu(), o["Sig_inv"]) < REL
+
+
+def test_reduce_partitions_and_determinism(torch_cuda, M):
+    from dlsa_amd.dlsa import reduce_partitions_device, split_reduced
+
+    p = 20
+    sizes = [3000] * 6
+    X, y = O.simulate_counter(sum(sizes), p, seed=11)
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    f1 = M.logistic_model_batched(X, y, off)
+    f2 = M.logistic_model_batched(X, y, off)
+    assert torch_cuda.equal(f1.theta, f2.theta) and torch_cuda.equal(f1.sig_inv, f2.sig_inv)
+    buf = reduce_partitions_device(f1).cpu().numpy()
+    S, v, st, K = split_reduced(buf, p)
+    assert K == 6
+    sig = f1.sig_inv.cpu().numpy()
+    acc = np.zeros_like(sig[0])
+    for k in range(6):
+        acc = acc + sig[k]
+    assert np.array_equal(S, acc)
+    assert _rel(v, f1.sig_inv_theta.cpu().numpy().sum(0)) < 1e-14
+    assert _rel(st, f1.theta.cpu().numpy().sum(0)) < 1e-14
+
+
+def test_config2_shape_sampled_partitions(torch_cuda, M):
+    """BASELINE config-2 geometry (p=100, n_k = 97 656) on 32 partitions
+    generated in HBM; 4 sampled partitions against the oracle, all partitions
+    through size-independent checks (status, Sig_inv symmetry / PD, score
+    equation X^T(y - mu) ~ 0 at theta)."""
+    torch = torch_cuda
+    K, nk, p = 32, 97656, 100
+    X, y = M.simulate_logistic_device(K * nk, p, seed=2019)
+    off = np.arange(K + 1, dtype=np.int64) * nk
+    fit = M.logistic_model_batched(X, y, off)
+    assert (fit.status.cpu().numpy() == 0).all()
+    S = fit.sig_inv
+    assert torch.allclose(S, S.transpose(1, 2), rtol=0, atol=0)
+    for k in (0, 7, 19, 31):
+        Xk = X[off[k]:off[k + 1]].cpu().numpy()
+        yk = y[off[k]:off[k + 1]].cpu().numpy()
+        o = O.logistic_fit(Xk, yk)
+        assert _rel(fit.theta[k].cpu(), o["coef"]) < REL
+        assert _rel(fit.sig_inv[k].cpu(), o["Sig_inv"]) < REL
+    # score equation on every partition, evaluated on the device in fp64
+    th = fit.theta
+    for k in range(K):
+        Xk = X[off[k]:off[k + 1]]
+        mu = torch.sigmoid(Xk @ th[k])
+        gk = Xk.T @ (y[off[k]:off[k + 1]] - mu)
+        assert gk.abs().max().item() < 1e-6
