@@ -165,13 +165,15 @@ int dlsa_last_fit_stats(dlsa_fit_stats* out) {
   return DLSA_OK;
 }
 
-int dlsa_logistic_fit_batched_ex(const double* X, const double* y, const int64_t* offsets,
-                                 int32_t K, int32_t p, int32_t fit_intercept,
-                                 const double* center, const double* scale, int32_t max_iter,
-                                 double tol, double* theta, double* sig_inv,
-                                 double* sig_inv_theta, double* loglik, int32_t* iters,
-                                 int32_t* status, const dlsa_fit_options* opt_in,
-                                 void* stream_) {
+}  // extern "C"
+
+namespace dlsa {
+
+static int fit_impl(int family, const double* X, const double* y, const int64_t* offsets,
+                    int32_t K, int32_t p, int32_t fit_intercept, const double* center,
+                    const double* scale, int32_t max_iter, double tol, double* theta,
+                    double* sig_inv, double* sig_inv_theta, double* loglik, int32_t* iters,
+                    int32_t* status, const dlsa_fit_options* opt_in, void* stream_) {
   const auto t_start = std::chrono::steady_clock::now();
   g_last_error.clear();
   memset(&g_stats, 0, sizeof(g_stats));
@@ -262,7 +264,9 @@ int dlsa_logistic_fit_batched_ex(const double* X, const double* y, const int64_t
                               hipMemcpyHostToDevice, stream));
   DLSA_HIP_TRY(hipMemcpyAsync(d_offsets, offsets, 8LL * (K + 1), hipMemcpyHostToDevice, stream));
 
-  const int start_phase = opt.hessian_mode == DLSA_HESSIAN_FP64 ? PHASE_F64 : PHASE_F32;
+  if (family == FAMILY_GAUSSIAN) max_iter = 1;  // closed form: one exact fp64 pass
+  const int start_phase =
+      (opt.hessian_mode == DLSA_HESSIAN_FP64 || family == FAMILY_GAUSSIAN) ? PHASE_F64 : PHASE_F32;
   DLSA_HIP_TRY(launch_fit_init(d_offsets, K, P, start_phase, theta, d_phase, d_bt, iters, status,
                                d_llprev, sig_inv, loglik, stream));
 
@@ -313,6 +317,7 @@ int dlsa_logistic_fit_batched_ex(const double* X, const double* y, const int64_t
   sa.loglik = loglik;
   sa.P = P;
   sa.NT = pl.NT;
+  sa.family = family;
   sa.tol = tol;
   sa.switch_tol = opt.switch_tol;
 
@@ -365,7 +370,7 @@ int dlsa_logistic_fit_batched_ex(const double* X, const double* y, const int64_t
       nslot = std::max(2, std::min(nslot, 4));
       pa.nslot = nslot;
       DLSA_HIP_TRY(timed(f64 ? &g_stats.ms_pass_fp64 : &g_stats.ms_pass_fp32, [&] {
-        return launch_irls_pass(pa, pl.NT, f64, standardize, pl.n_chunks, stream);
+        return launch_irls_pass(pa, pl.NT, f64, standardize, family, pl.n_chunks, stream);
       }));
       if (f64) {
         g_stats.passes_fp64++;
@@ -391,6 +396,48 @@ int dlsa_logistic_fit_batched_ex(const double* X, const double* y, const int64_t
                                                                t_start)
                          .count();
   return DLSA_OK;
+}
+
+}  // namespace dlsa
+
+extern "C" {
+
+int dlsa_logistic_fit_batched_ex(const double* X, const double* y, const int64_t* offsets,
+                                 int32_t K, int32_t p, int32_t fit_intercept,
+                                 const double* center, const double* scale, int32_t max_iter,
+                                 double tol, double* theta, double* sig_inv,
+                                 double* sig_inv_theta, double* loglik, int32_t* iters,
+                                 int32_t* status, const dlsa_fit_options* opt, void* stream) {
+  return fit_impl(FAMILY_LOGISTIC, X, y, offsets, K, p, fit_intercept, center, scale, max_iter,
+                  tol, theta, sig_inv, sig_inv_theta, loglik, iters, status, opt, stream);
+}
+
+int dlsa_ols_fit_batched(const double* X, const double* y, const int64_t* offsets, int32_t K,
+                         int32_t p, int32_t fit_intercept, const double* center,
+                         const double* scale, double* theta, double* sig_inv,
+                         double* sig_inv_theta, double* rss, int32_t* status,
+                         const dlsa_fit_options* opt, void* stream) {
+  dlsa_fit_options o;
+  if (opt)
+    o = *opt;
+  else
+    dlsa_fit_options_default(&o);
+  o.hessian_mode = DLSA_HESSIAN_FP64;
+  // the iteration count is always 1 for OLS and not part of this ABI: give
+  // the driver a throw-away device array for it
+  int32_t* d_iters = nullptr;
+  hipStream_t s = (hipStream_t)stream;
+  if (K > 0) {
+    hipError_t e = hipMallocAsync((void**)&d_iters, sizeof(int32_t) * K, s);
+    if (e != hipSuccess) {
+      set_error(std::string("hipMallocAsync: ") + hipGetErrorString(e));
+      return DLSA_E_HIP;
+    }
+  }
+  const int rc = fit_impl(FAMILY_GAUSSIAN, X, y, offsets, K, p, fit_intercept, center, scale, 1,
+                          1.0, theta, sig_inv, sig_inv_theta, rss, d_iters, status, &o, stream);
+  if (d_iters) (void)hipFreeAsync(d_iters, s);
+  return rc;
 }
 
 int dlsa_logistic_fit_batched(const double* X, const double* y, const int64_t* offsets,

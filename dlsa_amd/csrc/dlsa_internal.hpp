@@ -15,6 +15,7 @@ namespace dlsa {
 // is returned as Sig_inv; FP64 fits start in PHASE_F64.
 enum : int32_t { PHASE_F32 = 0, PHASE_F64 = 1, PHASE_DONE = 2 };
 enum : int32_t { STATUS_RUNNING = -1 };
+enum : int32_t { FAMILY_LOGISTIC = 0, FAMILY_GAUSSIAN = 1 };
 
 // Rows of X one wave stages per LDS slot (4 MFMA k-steps of 4 rows).
 constexpr int kRowsPerBlock = 8;
@@ -62,13 +63,14 @@ struct SolveArgs {
   double* loglik;       // [K] out
   int32_t P;
   int32_t NT;
+  int32_t family;  // FAMILY_LOGISTIC: Newton to tol; FAMILY_GAUSSIAN: one exact step
   double tol;
   double switch_tol;
 };
 
 // Launchers (defined in the .hip files).
 hipError_t launch_irls_pass(const PassArgs& a, int NT, bool f64, bool standardize,
-                            int n_chunks, hipStream_t s);
+                            int family, int n_chunks, hipStream_t s);
 int pass_slot_bytes(int NT);
 int pass_waves_per_cu(bool f64);
 hipError_t launch_newton_solve(const SolveArgs& a, int K, hipStream_t s);

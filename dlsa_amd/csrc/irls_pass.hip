@@ -55,11 +55,22 @@ __device__ __forceinline__ void wait_vmcnt_le(int n) {
   }
 }
 
+// DPP row_ror:n within each 16-lane row (dpp_ctrl 0x120 + n), on both halves
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+// Sum over the 16 lanes of a row; every lane ends with the bitwise-identical
+// total (each step adds a commutative pair), so all lanes of a row see the
+// same eta, w and r.
 __device__ __forceinline__ double red16(double v) {
-  v += __shfl_xor(v, 8, 16);
-  v += __shfl_xor(v, 4, 16);
-  v += __shfl_xor(v, 2, 16);
-  v += __shfl_xor(v, 1, 16);
+  v += dpp_f64<0x128>(v);
+  v += dpp_f64<0x124>(v);
+  v += dpp_f64<0x122>(v);
+  v += dpp_f64<0x121>(v);
   return v;
 }
 
@@ -83,7 +94,7 @@ struct Geom {
   static constexpr int T = NT * (NT + 1) / 2;
 };
 
-template <int NT, bool F64, bool STD>
+template <int NT, bool F64, bool STD, int FAM>
 __global__ __launch_bounds__(64, (F64 || NT >= 8) ? 1 : 2) void irls_pass_kernel(const PassArgs a) {
   using G = Geom<NT>;
   constexpr int T = G::T;
@@ -193,16 +204,30 @@ __global__ __launch_bounds__(64, (F64 || NT >= 8) ? 1 : 2) void irls_pass_kernel
       for (int c = 0; c < NT; ++c) e = fma(xf[c], beta[c], e);
       e = red16(e);  // eta of row rl, in all 16 lanes of the row
       const double yv = ysl[rl];
-      const double ea = exp(-fabs(e));
-      const double inv = 1.0 / (1.0 + ea);
-      const double mu = e >= 0.0 ? inv : ea * inv;
-      double w = ea * inv * inv;  // mu (1 - mu), cancellation free
-      double r = yv - mu;
+      double w, r;
+      if constexpr (FAM == FAMILY_LOGISTIC) {
+        const double ea = exp(-fabs(e));
+        const double inv = 1.0 / (1.0 + ea);
+        const double mu = e >= 0.0 ? inv : ea * inv;
+        w = ea * inv * inv;  // mu (1 - mu), cancellation free
+        r = yv - mu;
+        if (valid && fl == 0) {
+          // log-likelihood: exact fp64 in the fp64 pass (its value is
+          // returned); fp32 log in fp32-Hessian passes, where it only drives
+          // step halving (|error| < 1e-7 per row, far below the 1e-6 relative
+          // threshold of newton_solve_kernel)
+          const double sp = F64 ? log1p(ea) : (double)__logf(1.0f + (float)ea);
+          llacc += yv * e - (fmax(e, 0.0) + sp);
+        }
+      } else {  // gaussian (OLS): mu = eta, w = 1, ll = -rss/2
+        w = 1.0;
+        r = yv - e;
+        if (valid && fl == 0) llacc -= 0.5 * r * r;
+      }
       if (!valid) {
         w = 0.0;
         r = 0.0;
       }
-      if (valid && fl == 0) llacc += yv * e - (fmax(e, 0.0) + log1p(ea));
 #pragma unroll
       for (int c = 0; c < NT; ++c) gacc[c] = fma(xf[c], r, gacc[c]);
 
@@ -281,9 +306,9 @@ int pass_slot_bytes(int NT) {
 
 int pass_waves_per_cu(bool f64) { return f64 ? 4 : 8; }
 
-template <int NT, bool F64, bool STD>
+template <int NT, bool F64, bool STD, int FAM>
 static hipError_t launch_t(const PassArgs& a, int n_chunks, hipStream_t s) {
-  auto kern = irls_pass_kernel<NT, F64, STD>;
+  auto kern = irls_pass_kernel<NT, F64, STD, FAM>;
   const size_t lds = (size_t)a.nslot * a.slot_bytes;
   static bool attr_set = false;  // per instantiation
   if (!attr_set) {
@@ -297,22 +322,31 @@ static hipError_t launch_t(const PassArgs& a, int n_chunks, hipStream_t s) {
 }
 
 template <int NT>
-static hipError_t launch_nt(const PassArgs& a, bool f64, bool std_, int n_chunks, hipStream_t s) {
-  if (f64) return std_ ? launch_t<NT, true, true>(a, n_chunks, s) : launch_t<NT, true, false>(a, n_chunks, s);
-  return std_ ? launch_t<NT, false, true>(a, n_chunks, s) : launch_t<NT, false, false>(a, n_chunks, s);
+static hipError_t launch_nt(const PassArgs& a, bool f64, bool std_, int family, int n_chunks,
+                            hipStream_t s) {
+  if (family == FAMILY_GAUSSIAN) {  // OLS: a single exact pass, fp64 only
+    if (!f64) return hipErrorInvalidValue;
+    return std_ ? launch_t<NT, true, true, FAMILY_GAUSSIAN>(a, n_chunks, s)
+                : launch_t<NT, true, false, FAMILY_GAUSSIAN>(a, n_chunks, s);
+  }
+  if (f64)
+    return std_ ? launch_t<NT, true, true, FAMILY_LOGISTIC>(a, n_chunks, s)
+                : launch_t<NT, true, false, FAMILY_LOGISTIC>(a, n_chunks, s);
+  return std_ ? launch_t<NT, false, true, FAMILY_LOGISTIC>(a, n_chunks, s)
+              : launch_t<NT, false, false, FAMILY_LOGISTIC>(a, n_chunks, s);
 }
 
-hipError_t launch_irls_pass(const PassArgs& a, int NT, bool f64, bool standardize, int n_chunks,
-                            hipStream_t s) {
+hipError_t launch_irls_pass(const PassArgs& a, int NT, bool f64, bool standardize, int family,
+                            int n_chunks, hipStream_t s) {
   switch (NT) {
-    case 1: return launch_nt<1>(a, f64, standardize, n_chunks, s);
-    case 2: return launch_nt<2>(a, f64, standardize, n_chunks, s);
-    case 3: return launch_nt<3>(a, f64, standardize, n_chunks, s);
-    case 4: return launch_nt<4>(a, f64, standardize, n_chunks, s);
-    case 5: return launch_nt<5>(a, f64, standardize, n_chunks, s);
-    case 6: return launch_nt<6>(a, f64, standardize, n_chunks, s);
-    case 7: return launch_nt<7>(a, f64, standardize, n_chunks, s);
-    case 8: return launch_nt<8>(a, f64, standardize, n_chunks, s);
+    case 1: return launch_nt<1>(a, f64, standardize, family, n_chunks, s);
+    case 2: return launch_nt<2>(a, f64, standardize, family, n_chunks, s);
+    case 3: return launch_nt<3>(a, f64, standardize, family, n_chunks, s);
+    case 4: return launch_nt<4>(a, f64, standardize, family, n_chunks, s);
+    case 5: return launch_nt<5>(a, f64, standardize, family, n_chunks, s);
+    case 6: return launch_nt<6>(a, f64, standardize, family, n_chunks, s);
+    case 7: return launch_nt<7>(a, f64, standardize, family, n_chunks, s);
+    case 8: return launch_nt<8>(a, f64, standardize, family, n_chunks, s);
     default: return hipErrorInvalidValue;
   }
 }

@@ -225,6 +225,46 @@ def logistic_model_batched(X, y, offsets, fit_intercept=False, center=None, scal
     return BatchedFit(theta, sig, sigt, ll, iters, status, offs, bool(fit_intercept), stats)
 
 
+def ols_model_batched(X, y, offsets, fit_intercept=False, center=None, scale=None,
+                      rows_per_chunk=0, record_timing=False, device=None):
+    """Batched local OLS (linear DLSA path): per
+    partition theta_k = (X_k^T X_k)^-1 X_k^T y_k and Sig_inv_k = X_k^T X_k from
+    one fused fp64 pass.  Returns a BatchedFit whose ``loglik`` field holds the
+    residual sum of squares of each partition."""
+    dev = _require_gpu(device)
+    Xd = _dev_f64(X, dev)
+    yd = _dev_f64(y, dev).reshape(-1)
+    n, p = Xd.shape
+    offs = np.ascontiguousarray(np.asarray(offsets, dtype=np.int64))
+    K = offs.size - 1
+    if K < 1 or offs[0] != 0 or offs[-1] != n or np.any(np.diff(offs) < 0) or yd.numel() != n:
+        raise ValueError("offsets must be non-decreasing, start at 0 and end at n; y has n rows")
+    P = p + (1 if fit_intercept else 0)
+    if P > _hip.MAX_P_FUSED:
+        raise DlsaHipError(f"P = {P} > {_hip.MAX_P_FUSED} not supported by the fused pass yet")
+    cd = sd = None
+    if center is not None or scale is not None:
+        cd = _dev_f64(center, dev).reshape(-1)
+        sd = _dev_f64(scale, dev).reshape(-1)
+    theta = torch.empty((K, P), dtype=torch.float64, device=dev)
+    sig = torch.empty((K, P, P), dtype=torch.float64, device=dev)
+    sigt = torch.empty((K, P), dtype=torch.float64, device=dev)
+    rss = torch.empty((K,), dtype=torch.float64, device=dev)
+    status = torch.empty((K,), dtype=torch.int32, device=dev)
+    lib = _hip.load()
+    opt = _hip.default_options()
+    opt.rows_per_chunk = int(rows_per_chunk)
+    opt.record_timing = 1 if record_timing else 0
+    rc = lib.dlsa_ols_fit_batched(_ptr(Xd), _ptr(yd), offs.ctypes.data_as(ctypes.c_void_p), K, p,
+                                  int(bool(fit_intercept)), _ptr(cd), _ptr(sd), _ptr(theta),
+                                  _ptr(sig), _ptr(sigt), _ptr(rss), _ptr(status),
+                                  ctypes.byref(opt), _stream(dev))
+    _hip.check(rc, "dlsa_ols_fit_batched")
+    iters = torch.ones((K,), dtype=torch.int32, device=dev)
+    return BatchedFit(theta, sig, sigt, rss, iters, status, offs, bool(fit_intercept),
+                      _hip.last_fit_stats())
+
+
 # ---------------------------------------------------------------------------
 # reference-signature wrapper (one Spark group)
 # ---------------------------------------------------------------------------

@@ -136,6 +136,24 @@ int dlsa_logistic_fit_batched_ex(const double* X, const double* y,
                                  int32_t* iters, int32_t* status,
                                  const dlsa_fit_options* opt, void* stream);
 
+/*
+ * Batched local OLS fit (the linear DLSA path; the
+ * reference only has a statsmodels per-group demo,
+ * projects/results/linear_regression_dc.py:27-37):
+ *   theta_k = (X_k^T X_k)^-1 X_k^T y_k,  Sig_inv_k = X_k^T X_k,
+ *   sig_inv_theta_k = Sig_inv_k theta_k (= X_k^T y_k),
+ *   rss_k = sum (y - X theta_k)^2.
+ * One fused fp64 pass over X (same kernel as the logistic pass with w = 1)
+ * plus one per-partition Cholesky solve.  opt may be NULL; its hessian_mode
+ * is ignored (always fp64).
+ */
+int dlsa_ols_fit_batched(const double* X, const double* y, const int64_t* offsets,
+                         int32_t K, int32_t p, int32_t fit_intercept,
+                         const double* center, const double* scale, double* theta,
+                         double* sig_inv, double* sig_inv_theta, double* rss,
+                         int32_t* status, const dlsa_fit_options* opt,
+                         void* stream);
+
 /* Timing/iteration record of the calling thread's last fit. */
 int dlsa_last_fit_stats(dlsa_fit_stats* out);
 

@@ -230,3 +230,26 @@ def test_config2_shape_sampled_partitions(torch_cuda, M):
         mu = torch.sigmoid(Xk @ th[k])
         gk = Xk.T @ (y[off[k]:off[k + 1]] - mu)
         assert gk.abs().max().item() < 1e-6
+
+
+@pytest.mark.parametrize("p,fi", [(8, True), (64, False), (100, True)])
+def test_ols_vs_oracle(torch_cuda, M, p, fi):
+    """Linear DLSA path (config 4 shape at small n): closed-form OLS per
+    partition, Sig_inv = X^T X, rss."""
+    rs = np.random.RandomState(p)
+    sizes = [4000, 2501, 3333]
+    n = sum(sizes)
+    X = rs.rand(n, p) - 0.5
+    y = X @ rs.randn(p) + 0.3 + 0.1 * rs.randn(n)
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    fit = M.ols_model_batched(X, y, off, fit_intercept=fi, rows_per_chunk=900)
+    assert (fit.status.cpu().numpy() == 0).all()
+    for k in range(3):
+        o = O.ols_fit(X[off[k]:off[k + 1]], y[off[k]:off[k + 1]], fit_intercept=fi)
+        assert _rel(fit.theta[k].cpu(), o["coef"]) < REL
+        assert _rel(fit.sig_inv[k].cpu(), o["Sig_inv"]) < 1e-12
+        Xk = X[off[k]:off[k + 1]]
+        if fi:
+            Xk = np.column_stack([np.ones(len(Xk)), Xk])
+        rss = float(((y[off[k]:off[k + 1]] - Xk @ o["coef"]) ** 2).sum())
+        assert abs(fit.loglik[k].item() - rss) < 1e-6 * rss
