@@ -54,9 +54,11 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
     const int gi = 16 * I + (within >> 4), gj = 16 * J + (within & 15);
     double s = 0.0;
     for (int c = cb; c < ce; ++c) s += a.slab_H[((int64_t)c * T + t) * 256 + within];
-    if (gi < P && gj < P) {
+    // lower triangle only (diagonal tiles hold (w x_i) x_j and (w x_j) x_i,
+    // which differ in the last bit): mirroring makes Sig_inv exactly symmetric
+    if (gi < P && gj < P && gi >= gj) {
       H[gi * LD + gj] = s;
-      if (I != J) H[gj * LD + gi] = s;
+      H[gj * LD + gi] = s;
     }
   }
   for (int f = tid; f < P; f += 256) {
