@@ -38,21 +38,21 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
+def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()) -> str:
+    if not force and out == OUT and not _stale():
         return OUT
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wall", "-Wno-unused-function", "-Wno-unused-command-line-argument",
-           "-I" + os.path.join(ROOT, "include"),
-           *[os.path.join(CSRC, s) for s in SOURCES], "-o", OUT + ".tmp"]
+           "-I" + os.path.join(ROOT, "include"), *[f"-D{d}" for d in defines],
+           *[os.path.join(CSRC, s) for s in SOURCES], "-o", out + ".tmp"]
     if verbose:
         print(" ".join(cmd), flush=True)
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         sys.stderr.write(res.stdout + res.stderr)
         raise RuntimeError(f"hipcc failed ({res.returncode})")
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 def main(argv=None):

@@ -1,6 +1,7 @@
 // extern "C" entry points of libdlsa_hip.so (declared in include/dlsa_hip.h)
 // and the host side of the batched Newton/IRLS driver.
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -365,9 +366,11 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
       if (n_running[ph] == 0) continue;
       const bool f64 = ph == PHASE_F64;
       pa.want_phase = ph;
-      const int waves = pass_waves_per_cu(f64);
-      int nslot = (160 * 1024 / waves) / pa.slot_bytes;
+      int waves = pass_waves_per_cu(f64);
+      if (const char* e = getenv(f64 ? "DLSA_WAVES_F64" : "DLSA_WAVES_F32")) waves = atoi(e);
+      int nslot = (160 * 1024 / std::max(waves, 1)) / pa.slot_bytes;
       nslot = std::max(2, std::min(nslot, 4));
+      if (const char* e = getenv("DLSA_NSLOT")) nslot = std::max(2, std::min(atoi(e), 4));
       pa.nslot = nslot;
       DLSA_HIP_TRY(timed(f64 ? &g_stats.ms_pass_fp64 : &g_stats.ms_pass_fp32, [&] {
         return launch_irls_pass(pa, pl.NT, f64, standardize, family, pl.n_chunks, stream);

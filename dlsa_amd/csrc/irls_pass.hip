@@ -78,6 +78,13 @@ __device__ __forceinline__ int npieces_for(int p) {
   return (kRowsPerBlock * p * 8 + 16 + 1023) / 1024;
 }
 
+// Profiling-only ablations (tools/build_variants.sh builds them as separate
+// .so files; the product build has DLSA_ABLATE = 0):
+//   1 = no MFMA, 2 = no transcendentals, 3 = stream only (DMA ring, no math)
+#ifndef DLSA_ABLATE
+#define DLSA_ABLATE 0
+#endif
+
 template <int NT>
 struct Geom {
   static constexpr int PMAX = 16 * NT;
@@ -185,6 +192,10 @@ __global__ __launch_bounds__(64, (F64 || NT >= 8) ? 1 : 2) void irls_pass_kernel
     const double* xs = (const double*)(slot + G::PAD + (start & 15));
     const double* ysl = (const double*)(slot + G::SLOT_X);
     const int rows_left = nrows - b * RB;
+    if constexpr (DLSA_ABLATE == 3) {
+      llacc += xs[lane] + ysl[lane & 7];
+      continue;
+    }
 
 #pragma unroll
     for (int s = 0; s < RB / 4; ++s) {
@@ -205,7 +216,11 @@ __global__ __launch_bounds__(64, (F64 || NT >= 8) ? 1 : 2) void irls_pass_kernel
       e = red16(e);  // eta of row rl, in all 16 lanes of the row
       const double yv = ysl[rl];
       double w, r;
-      if constexpr (FAM == FAMILY_LOGISTIC) {
+      if constexpr (FAM == FAMILY_LOGISTIC && DLSA_ABLATE == 2) {
+        w = 0.25 - 0.01 * e * e;
+        r = yv - 0.5 - 0.2 * e;
+        if (valid && fl == 0) llacc += yv * e;
+      } else if constexpr (FAM == FAMILY_LOGISTIC) {
         const double ea = exp(-fabs(e));
         const double inv = 1.0 / (1.0 + ea);
         const double mu = e >= 0.0 ? inv : ea * inv;
@@ -231,7 +246,13 @@ __global__ __launch_bounds__(64, (F64 || NT >= 8) ? 1 : 2) void irls_pass_kernel
 #pragma unroll
       for (int c = 0; c < NT; ++c) gacc[c] = fma(xf[c], r, gacc[c]);
 
-      if constexpr (F64) {
+      if constexpr (DLSA_ABLATE == 1) {
+#pragma unroll
+        for (int c = 0; c < NT; ++c) {
+          float af = (float)(xf[c] * w);
+          asm volatile("" ::"v"(af));
+        }
+      } else if constexpr (F64) {
         double af[NT];
 #pragma unroll
         for (int c = 0; c < NT; ++c) af[c] = xf[c] * w;

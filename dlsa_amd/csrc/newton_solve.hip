@@ -29,13 +29,22 @@ __device__ __forceinline__ double block_max(double v, double* red) {
   return r;
 }
 
+// Sum of 64 lanes, result in every lane.
+__device__ __forceinline__ double wave_sum(double v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+template <int NT>
 __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
+  constexpr int T = NT * (NT + 1) / 2;
+  constexpr int PP = 16 * NT;
   const int k = blockIdx.x;
   const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
   if (a.status[k] != STATUS_RUNNING) return;  // block-uniform
-  const int P = a.P, NT = a.NT, PP = 16 * NT;
-  const int T = NT * (NT + 1) / 2;
+  const int P = a.P;
   const int LD = P + 1;
   double* H = sm;            // P x LD
   double* g = H + P * LD;    // PP
@@ -45,31 +54,43 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
   const int cb = a.part_chunk_begin[k], ce = a.part_chunk_begin[k + 1];
   const int phase = a.phase[k];
 
-  // 1. assemble ------------------------------------------------------------
-  for (int e = tid; e < T * 256; e += 256) {
-    const int t = e >> 8, within = e & 255;
-    int I = 0;
-    while ((I + 1) * (I + 2) / 2 <= t) ++I;
-    const int J = t - I * (I + 1) / 2;
-    const int gi = 16 * I + (within >> 4), gj = 16 * J + (within & 15);
-    double s = 0.0;
-    for (int c = cb; c < ce; ++c) s += a.slab_H[((int64_t)c * T + t) * 256 + within];
-    // lower triangle only (diagonal tiles hold (w x_i) x_j and (w x_j) x_i,
-    // which differ in the last bit): mirroring makes Sig_inv exactly symmetric
-    if (gi < P && gj < P && gi >= gj) {
-      H[gi * LD + gj] = s;
-      H[gj * LD + gi] = s;
+  // 1. assemble: thread tid owns element (tile t, position tid) of every
+  //    tile; the chunk loop issues T independent loads per step
+  {
+    double acc[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) acc[t] = 0.0;
+    for (int c = cb; c < ce; ++c) {
+      const double* src = a.slab_H + (int64_t)c * T * 256 + tid;
+#pragma unroll
+      for (int t = 0; t < T; ++t) acc[t] += src[t * 256];
     }
+    const int r = tid >> 4, q = tid & 15;
+#pragma unroll
+    for (int I = 0; I < NT; ++I)
+#pragma unroll
+      for (int J = 0; J <= I; ++J) {
+        const int t = I * (I + 1) / 2 + J;
+        const int gi = 16 * I + r, gj = 16 * J + q;
+        // lower triangle only (diagonal tiles hold (w x_i) x_j and
+        // (w x_j) x_i, equal up to the last bit): mirroring makes Sig_inv
+        // exactly symmetric
+        if (gi < P && gj < P && gi >= gj) {
+          H[gi * LD + gj] = acc[t];
+          H[gj * LD + gi] = acc[t];
+        }
+      }
   }
-  for (int f = tid; f < P; f += 256) {
+  if (tid < PP) {
     double s = 0.0;
-    for (int c = cb; c < ce; ++c) s += a.slab_g[(int64_t)c * PP + f];
-    g[f] = s;
+    for (int c = cb; c < ce; ++c) s += a.slab_g[(int64_t)c * PP + tid];
+    g[tid] = s;
   }
-  if (tid == 0) {
+  if (wid == 0) {
     double s = 0.0;
-    for (int c = cb; c < ce; ++c) s += a.slab_ll[c];
-    red[7] = s;
+    for (int c = cb + lane; c < ce; c += 64) s += a.slab_ll[c];
+    s = wave_sum(s);
+    if (lane == 0) red[7] = s;
   }
   __syncthreads();
   const double ll = red[7];
@@ -82,10 +103,11 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
   }
 
   // 2. step halving on a log-likelihood decrease ---------------------------
+  //    threshold above the fp32-log noise of mixed-mode log-likelihoods; real
+  //    overshoots of a Newton step lose far more than 1e-6 relative
   const double llp = a.ll_prev[k];
-  // threshold above the fp32-log noise of mixed-mode log-likelihoods; real
-  // overshoots of a Newton step lose far more than 1e-6 relative
-  if (it > 0 && ll < llp - 1e-6 * (1.0 + fabs(llp)) && a.backtracks[k] < 40) {
+  if (a.family == FAMILY_LOGISTIC && it > 0 && ll < llp - 1e-6 * (1.0 + fabs(llp)) &&
+      a.backtracks[k] < 40) {
     const int bt = a.backtracks[k] + 1;
     const double sc = ldexp(1.0, -bt);
     const double* tp = a.theta_prev + (int64_t)k * P;
@@ -101,33 +123,50 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
 
   // 3. publish the information matrix at the evaluation point --------------
   double* S = a.sig_inv + (int64_t)k * P * P;
-  for (int e = tid; e < P * P; e += 256) S[e] = H[(e / P) * LD + (e % P)];
+  for (int e = tid; e < P * P; e += 256) {
+    const int i = e / P;
+    S[e] = H[i * LD + (e - i * P)];
+  }
   if (tid == 0) a.loglik[k] = ll;
-
-  // 4. Cholesky (right-looking, lower, in place) ---------------------------
-  if (tid == 0) red[6] = 1.0;
   __syncthreads();
+
+  // 4. Cholesky, right-looking, lower, in place.  Thread (row = tid/2,
+  //    parity = tid%2) owns the even/odd columns of one row.  Column j is
+  //    only READ during step j (l_xj = H[x][j] / sqrt(H[j][j]) recomputed by
+  //    every reader); its scaled values are written back at step j+1, so one
+  //    barrier per column suffices.
+  const int row = tid >> 1, par = tid & 1;
+  bool ok = true;
+  double inv_prev = 0.0;
   for (int j = 0; j < P; ++j) {
-    if (tid == 0) {
-      const double d = H[j * LD + j];
-      if (!(d > 0.0) || !isfinite(d)) red[6] = 0.0;
-      else H[j * LD + j] = sqrt(d);
+    const double d = H[j * LD + j];
+    if (!(d > 0.0) || !isfinite(d)) {
+      ok = false;  // uniform: every thread read the same d
+      break;
     }
-    __syncthreads();
-    if (red[6] == 0.0) break;
-    const double djj = H[j * LD + j];
-    for (int i = j + 1 + tid; i < P; i += 256) H[i * LD + j] /= djj;
-    __syncthreads();
-    const int n = P - j - 1;
-    for (int e = tid; e < n * n; e += 256) {
-      const int i = j + 1 + e / n, c = j + 1 + e % n;
-      if (c <= i) H[i * LD + c] -= H[i * LD + j] * H[c * LD + j];
+    const double ljj = sqrt(d);
+    const double inv = 1.0 / ljj;
+    if (row < P && par == 0 && j > 0 && row >= j - 1) {
+      // deferred write-back of column j-1 (scaled) for this row
+      H[row * LD + (j - 1)] = (row == j - 1) ? sqrt(H[row * LD + row]) : H[row * LD + (j - 1)] * inv_prev;
     }
+    if (row < P && row > j) {
+      const double lij = H[row * LD + j] * inv;
+      for (int c = j + 1 + par; c <= row; c += 2)
+        H[row * LD + c] -= lij * (H[c * LD + j] * inv);
+    }
+    inv_prev = inv;
     __syncthreads();
   }
-  if (red[6] == 0.0) {
+  if (ok && row < P && par == 0 && row >= P - 1) {
+    // last column: only the diagonal element
+    H[row * LD + row] = sqrt(H[row * LD + row]);
+  }
+  __syncthreads();
+  if (!ok) {
     if (tid == 0) {
-      if (phase == PHASE_F32) {  // fp32 Hessian lost definiteness: redo in fp64
+      if (phase == PHASE_F32 && a.family == FAMILY_LOGISTIC) {
+        // fp32 Hessian lost definiteness: redo this point with fp64
         a.phase[k] = PHASE_F64;
         a.iters[k] = it + 1;
         atomicAdd(&a.counters[PHASE_F64], 1);
@@ -138,26 +177,34 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
     return;
   }
 
-  // 5. solve L z = g, L^T d = z (d overwrites z) ---------------------------
-  for (int f = tid; f < PP; f += 256) z[f] = f < P ? g[f] : 0.0;
+  // 5. triangular solves L z = g, L^T d = z by wave 0 (no barriers: lane l
+  //    holds z[l] and z[l+64]; the pivot is broadcast by shuffle)
+  if (wid == 0) {
+    double z0 = lane < P ? g[lane] : 0.0;
+    double z1 = lane + 64 < P ? g[lane + 64] : 0.0;
+    for (int j = 0; j < P; ++j) {
+      const double zj = __shfl(j < 64 ? z0 : z1, j & 63) / H[j * LD + j];
+      if (lane == (j & 63)) {
+        if (j < 64) z0 = zj; else z1 = zj;
+      }
+      if (lane > j && lane < P) z0 -= H[lane * LD + j] * zj;
+      if (lane + 64 > j && lane + 64 < P) z1 -= H[(lane + 64) * LD + j] * zj;
+    }
+    for (int j = P - 1; j >= 0; --j) {
+      const double zj = __shfl(j < 64 ? z0 : z1, j & 63) / H[j * LD + j];
+      if (lane == (j & 63)) {
+        if (j < 64) z0 = zj; else z1 = zj;
+      }
+      if (lane < j) z0 -= H[j * LD + lane] * zj;
+      if (lane + 64 < j) z1 -= H[j * LD + lane + 64] * zj;
+    }
+    if (lane < P) z[lane] = z0;
+    if (lane + 64 < P) z[lane + 64] = z1;
+  }
   __syncthreads();
-  for (int j = 0; j < P; ++j) {
-    if (tid == 0) z[j] /= H[j * LD + j];
-    __syncthreads();
-    const double zj = z[j];
-    for (int i = j + 1 + tid; i < P; i += 256) z[i] -= H[i * LD + j] * zj;
-    __syncthreads();
-  }
-  for (int j = P - 1; j >= 0; --j) {
-    if (tid == 0) z[j] /= H[j * LD + j];
-    __syncthreads();
-    const double zj = z[j];
-    for (int i = tid; i < j; i += 256) z[i] -= H[j * LD + i] * zj;
-    __syncthreads();
-  }
 
   // 6. update + convergence ------------------------------------------------
-  double dm = 0.0, tm = 0.0;
+  double dm = 0.0, tm = 0.0, tg = 0.0;
   double* tp = a.theta_prev + (int64_t)k * P;
   double* dp = a.delta_prev + (int64_t)k * P;
   for (int f = tid; f < P; f += 256) {
@@ -169,21 +216,19 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
     th[f] = t1;
     dm = fmax(dm, fabs(d));
     tm = fmax(tm, fabs(t1));
+    tg += t1 * g[f];
   }
   dm = block_max(dm, red);
   tm = block_max(tm, red);
   if (a.family == FAMILY_GAUSSIAN) {
     // OLS: theta was 0, one Newton step is the closed form (X^T X)^-1 X^T y;
     // residual sum of squares = y^T y - theta^T X^T y = -2 ll(0) - theta . g
-    double tg = 0.0;
-    for (int f = tid; f < P; f += 256) tg += th[f] * g[f];
-    for (int o = 32; o > 0; o >>= 1) tg += __shfl_xor(tg, o);
+    tg = wave_sum(tg);
     __syncthreads();
-    if ((tid & 63) == 0) red[tid >> 6] = tg;
+    if (lane == 0) red[wid] = tg;
     __syncthreads();
     if (tid == 0) {
-      const double s = red[0] + red[1] + red[2] + red[3];
-      a.loglik[k] = -2.0 * ll - s;
+      a.loglik[k] = -2.0 * ll - (red[0] + red[1] + red[2] + red[3]);
       a.iters[k] = it + 1;
       a.status[k] = isfinite(dm) ? DLSA_STATUS_OK : DLSA_STATUS_NONFINITE;
       a.phase[k] = PHASE_DONE;
@@ -211,18 +256,33 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
   }
 }
 
-hipError_t launch_newton_solve(const SolveArgs& a, int K, hipStream_t s) {
-  const int PP = 16 * a.NT;
-  const size_t lds = ((size_t)a.P * (a.P + 1) + 2 * PP + 8) * sizeof(double);
+template <int NT>
+static hipError_t launch_solve_t(const SolveArgs& a, int K, size_t lds, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)newton_solve_kernel,
+    hipError_t e = hipFuncSetAttribute((const void*)newton_solve_kernel<NT>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL(newton_solve_kernel, dim3(K), dim3(256), lds, s, a);
+  hipLaunchKernelGGL(newton_solve_kernel<NT>, dim3(K), dim3(256), lds, s, a);
   return hipGetLastError();
+}
+
+hipError_t launch_newton_solve(const SolveArgs& a, int K, hipStream_t s) {
+  const int PP = 16 * a.NT;
+  const size_t lds = ((size_t)a.P * (a.P + 1) + 2 * PP + 8) * sizeof(double);
+  switch (a.NT) {
+    case 1: return launch_solve_t<1>(a, K, lds, s);
+    case 2: return launch_solve_t<2>(a, K, lds, s);
+    case 3: return launch_solve_t<3>(a, K, lds, s);
+    case 4: return launch_solve_t<4>(a, K, lds, s);
+    case 5: return launch_solve_t<5>(a, K, lds, s);
+    case 6: return launch_solve_t<6>(a, K, lds, s);
+    case 7: return launch_solve_t<7>(a, K, lds, s);
+    case 8: return launch_solve_t<8>(a, K, lds, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 }  // namespace dlsa
