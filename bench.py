@@ -151,41 +151,43 @@ def main():
     ms64 = sum(s["ms_pass_fp64"] for s in stats_acc)
     n32 = sum(s["passes_fp32"] for s in stats_acc)
     n64 = sum(s["passes_fp64"] for s in stats_acc)
+    rows32 = sum(s["rows_fp32"] for s in stats_acc)
+    rows64 = sum(s["rows_fp64"] for s in stats_acc)
     ms_solve = sum(s["ms_solve"] for s in stats_acc)
-    bytes_per_pass = n * (8 * p + 8)
+    row_bytes = 8 * p + 8                       # X row + y, read once per pass
+    bytes_per_pass = n * row_bytes
     NT = (p + 15) // 16
     tiles = NT * (NT + 1) // 2
-    mfma_flops_per_pass = (n / 4.0) * tiles * (16 * 16 * 4 * 2)
+    mfma_flops_per_row = tiles * 16 * 16 * 2    # lower-triangle 16x16 tiles
     alg_flops_per_pass = n * (p * (p + 1) + 4 * p + 20)
     kern = {}
     if n32:
-        avg = ms32 / n32
-        kern["irls_pass_fp32hess"] = {
-            "launches_per_step": n32 / args.steps, "avg_ms": avg,
-            "GBps": bytes_per_pass / (avg * 1e-3) / 1e9,
-            "mfma_TFps": mfma_flops_per_pass / (avg * 1e-3) / 1e12}
+        kern["irls_coop<bf16 Hessian>"] = {
+            "launches_per_step": n32 / args.steps, "ms_per_step": ms32 / args.steps,
+            "avg_launch_ms": ms32 / n32, "rows_per_launch": rows32 / n32,
+            "GBps": rows32 * row_bytes / (ms32 * 1e-3) / 1e9,
+            "mfma_TFps": rows32 * mfma_flops_per_row / (ms32 * 1e-3) / 1e12}
     if n64:
-        avg = ms64 / n64
-        kern["irls_pass_fp64hess"] = {
-            "launches_per_step": n64 / args.steps, "avg_ms": avg,
-            "GBps": bytes_per_pass / (avg * 1e-3) / 1e9,
-            "mfma_TFps": mfma_flops_per_pass / (avg * 1e-3) / 1e12}
-    kern["newton_solve"] = {"launches_per_step": (n32 + n64) / args.steps / max(1, 1),
-                            "ms_per_step": ms_solve / args.steps}
+        kern["irls_coop<fp64 Hessian>"] = {
+            "launches_per_step": n64 / args.steps, "ms_per_step": ms64 / args.steps,
+            "avg_launch_ms": ms64 / n64, "rows_per_launch": rows64 / n64,
+            "GBps": rows64 * row_bytes / (ms64 * 1e-3) / 1e9,
+            "mfma_TFps": rows64 * mfma_flops_per_row / (ms64 * 1e-3) / 1e12}
+    kern["newton_solve"] = {"ms_per_step": ms_solve / args.steps}
     if ms32 >= ms64:
-        avg = ms32 / n32
-        achieved = bytes_per_pass / (avg * 1e-3) / 1e9
-        roof = {"kernel": "irls_pass_kernel<NT,fp32 Hessian>", "bound": "hbm",
-                "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        achieved = rows32 * row_bytes / (ms32 * 1e-3) / 1e9
+        roof = {"kernel": "irls_coop_kernel<NT=7,bf16 Hessian> (approximate-Hessian passes)",
+                "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                "algorithmic_bytes_per_launch": bytes_per_pass, "avg_launch_ms": avg}
+                "algorithmic_bytes_per_launch": rows32 * row_bytes / n32,
+                "avg_launch_ms": ms32 / n32}
     else:
-        avg = ms64 / n64
-        achieved = mfma_flops_per_pass / (avg * 1e-3) / 1e12
-        roof = {"kernel": "irls_pass_kernel<NT,fp64 Hessian>", "bound": "mfma",
+        achieved = rows64 * mfma_flops_per_row / (ms64 * 1e-3) / 1e12
+        roof = {"kernel": "irls_coop_kernel<NT=7,fp64 Hessian> (final pass)", "bound": "mfma",
                 "achieved": achieved, "peak": FP64_MFMA_PEAK_TF, "unit": "TFLOP/s",
                 "frac": achieved / FP64_MFMA_PEAK_TF, "traffic": None,
-                "mfma_flops_per_launch": mfma_flops_per_pass, "avg_launch_ms": avg}
+                "mfma_flops_per_launch": rows64 * mfma_flops_per_row / n64,
+                "avg_launch_ms": ms64 / n64}
     pmc_file = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_file):
         try:

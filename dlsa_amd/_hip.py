@@ -20,6 +20,7 @@ DLSA_OK = 0
 STATUS_NAMES = {0: "ok", 1: "maxiter", 2: "singular", 3: "empty", 4: "nonfinite"}
 HESSIAN_MIXED = 0
 HESSIAN_FP64 = 1
+HESSIAN_MIXED_F32 = 2
 MAX_P_FUSED = 128
 
 
@@ -35,7 +36,8 @@ class FitOptions(ctypes.Structure):
         ("workspace", ctypes.c_void_p),
         ("workspace_bytes", ctypes.c_int64),
         ("rows_per_chunk", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 7),
+        ("warm_start", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 6),
     ]
 
 

@@ -34,6 +34,33 @@ hipError_t launch_fit_init(const int64_t* offsets_dev, int K, int P, int start_p
   return hipGetLastError();
 }
 
+// Start of a warm-start level: running partitions re-enter the Newton loop
+// (the log-likelihood scale changes with the row count), non-finite iterates
+// restart from 0; counters[phase] = partitions running.
+__global__ void level_reset_kernel(int K, int P, int start_phase, int32_t* phase,
+                                   int32_t* status, double* ll_prev, int32_t* backtracks,
+                                   double* theta, int32_t* counters) {
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < K; k += gridDim.x * blockDim.x) {
+    if (status[k] != STATUS_RUNNING) continue;
+    bool finite = true;
+    for (int f = 0; f < P; ++f) finite &= (bool)isfinite(theta[(int64_t)k * P + f]);
+    if (!finite)
+      for (int f = 0; f < P; ++f) theta[(int64_t)k * P + f] = 0.0;
+    phase[k] = start_phase;
+    ll_prev[k] = -INFINITY;
+    backtracks[k] = 0;
+    atomicAdd(&counters[start_phase], 1);
+  }
+}
+
+hipError_t launch_level_reset(int K, int P, int start_phase, int32_t* phase, int32_t* status,
+                              double* ll_prev, int32_t* backtracks, double* theta,
+                              int32_t* counters, hipStream_t s) {
+  hipLaunchKernelGGL(level_reset_kernel, dim3((K + 255) / 256), dim3(256), 0, s, K, P,
+                     start_phase, phase, status, ll_prev, backtracks, theta, counters);
+  return hipGetLastError();
+}
+
 // sig_inv_theta = Sig_inv @ theta (models.py:131); still-running -> MAXITER.
 __global__ void fit_finalize_kernel(int K, int P, const double* theta, const double* sig_inv,
                                     double* sig_inv_theta, int32_t* status) {

@@ -40,15 +40,30 @@ struct Plan {
   std::vector<int32_t> chunk_rows, chunk_part, part_chunk_begin;
 };
 
+static bool use_perwave_pass() {
+  const char* e = getenv("DLSA_PASS");
+  return e && strcmp(e, "perwave") == 0;
+}
+
 static int auto_rows_per_chunk(int64_t n_total) {
-  // target ~8 waves per CU-slot round on 256 CUs
-  int64_t r = n_total / 4096;
-  r = std::max<int64_t>(256, std::min<int64_t>(r, 8192));
+  if (use_perwave_pass()) {
+    // one wave per chunk: ~8 waves per CU-slot round on 256 CUs
+    int64_t r = n_total / 4096;
+    r = std::max<int64_t>(256, std::min<int64_t>(r, 8192));
+    return (int)r;
+  }
+  // one 4-wave workgroup per chunk: ~4 rounds of 256 workgroups, so a
+  // partition of ~1e5 rows is one chunk at config 2 and small fits still
+  // spread over the CUs
+  int64_t r = n_total / 1024;
+  r = std::max<int64_t>(1024, std::min<int64_t>(r, 131072));
   return (int)r;
 }
 
+// rows_used(k) = clamp(ceil(frac * n_k), min_rows, n_k): a prefix of each
+// partition (frac = 1: all rows).
 static bool make_plan(const int64_t* offsets, int K, int p, int intercept, int rows_per_chunk,
-                      Plan& pl) {
+                      Plan& pl, double frac = 1.0, int64_t min_rows = 0) {
   pl.P = p + (intercept ? 1 : 0);
   pl.NT = (pl.P + 15) / 16;
   pl.T = pl.NT * (pl.NT + 1) / 2;
@@ -61,8 +76,10 @@ static bool make_plan(const int64_t* offsets, int K, int p, int intercept, int r
   pl.chunk_part.clear();
   for (int k = 0; k < K; ++k) {
     pl.part_chunk_begin[k] = (int32_t)pl.chunk_row0.size();
-    const int64_t a = offsets[k], b = offsets[k + 1];
-    const int64_t n = b - a;
+    const int64_t a = offsets[k];
+    const int64_t nk = offsets[k + 1] - a;
+    int64_t n = nk;
+    if (frac < 1.0) n = std::min(nk, std::max(min_rows, (int64_t)std::ceil(frac * (double)nk)));
     if (n <= 0) continue;
     const int64_t nc = (n + rpc - 1) / rpc;
     for (int64_t c = 0; c < nc; ++c) {
@@ -143,13 +160,14 @@ void dlsa_fit_options_default(dlsa_fit_options* opt) {
   memset(opt, 0, sizeof(*opt));
   opt->hessian_mode = DLSA_HESSIAN_MIXED;
   opt->switch_tol = 1e-6;
+  opt->warm_start = 1;
 }
 
 const char* dlsa_last_error(void) { return g_last_error.c_str(); }
 
 const char* dlsa_build_info(void) {
-  return "libdlsa_hip gfx950 (CDNA4): fused IRLS pass (LDS-DMA ring, f64/f32 16x16x4 MFMA), "
-         "LDS Cholesky Newton update, host LARS";
+  return "libdlsa_hip gfx950 (CDNA4): cooperative fused IRLS pass (shared LDS-DMA ring, "
+         "bf16 16x16x32 / f64 16x16x4 MFMA), LDS Cholesky Newton update, host LARS";
 }
 
 int64_t dlsa_logistic_workspace_bytes(const int64_t* offsets, int32_t K, int32_t p,
@@ -253,17 +271,44 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
   double* d_dprev = (double*)at(L.off_dprev);
   int32_t* d_cnt = (int32_t*)at(L.off_counters);
 
-  if (pl.n_chunks > 0) {
-    DLSA_HIP_TRY(hipMemcpyAsync(d_row0, pl.chunk_row0.data(), 8LL * pl.n_chunks,
-                                hipMemcpyHostToDevice, stream));
-    DLSA_HIP_TRY(hipMemcpyAsync(d_rows, pl.chunk_rows.data(), 4LL * pl.n_chunks,
-                                hipMemcpyHostToDevice, stream));
-    DLSA_HIP_TRY(hipMemcpyAsync(d_part, pl.chunk_part.data(), 4LL * pl.n_chunks,
-                                hipMemcpyHostToDevice, stream));
-  }
-  DLSA_HIP_TRY(hipMemcpyAsync(d_pcb, pl.part_chunk_begin.data(), 4LL * (K + 1),
-                              hipMemcpyHostToDevice, stream));
+  auto upload = [&](const Plan& q) -> hipError_t {
+    hipError_t e = hipSuccess;
+    if (q.n_chunks > 0) {
+      e = hipMemcpyAsync(d_row0, q.chunk_row0.data(), 8LL * q.n_chunks, hipMemcpyHostToDevice,
+                         stream);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(d_rows, q.chunk_rows.data(), 4LL * q.n_chunks,
+                           hipMemcpyHostToDevice, stream);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(d_part, q.chunk_part.data(), 4LL * q.n_chunks,
+                           hipMemcpyHostToDevice, stream);
+    }
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(d_pcb, q.part_chunk_begin.data(), 4LL * (K + 1), hipMemcpyHostToDevice,
+                         stream);
+    return e;
+  };
   DLSA_HIP_TRY(hipMemcpyAsync(d_offsets, offsets, 8LL * (K + 1), hipMemcpyHostToDevice, stream));
+
+  // warm-start levels: Newton on row prefixes (1/16, 1/4) before all rows
+  std::vector<Plan> plans;
+  if (family == FAMILY_LOGISTIC && opt.warm_start) {
+    const int64_t min_rows = std::max<int64_t>(2048, 64LL * pl.P);
+    for (double frac : {1.0 / 16.0, 1.0 / 4.0}) {
+      Plan q;
+      make_plan(offsets, K, p, fit_intercept, opt.rows_per_chunk, q, frac, min_rows);
+      int64_t rows = 0;
+      for (int c = 0; c < q.n_chunks; ++c) rows += q.chunk_rows[c];
+      if (rows <= n_total / 2 && q.n_chunks > 0) plans.push_back(std::move(q));
+    }
+  }
+  plans.push_back(pl);
+  std::vector<int64_t> plan_rows;
+  for (const Plan& q : plans) {
+    int64_t rows = 0;
+    for (int c = 0; c < q.n_chunks; ++c) rows += q.chunk_rows[c];
+    plan_rows.push_back(rows);
+  }
 
   if (family == FAMILY_GAUSSIAN) max_iter = 1;  // closed form: one exact fp64 pass
   const int start_phase =
@@ -297,7 +342,9 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
   pa.p = p;
   pa.P = P;
   pa.intercept = fit_intercept ? 1 : 0;
-  pa.slot_bytes = pass_slot_bytes(pl.NT);
+  const bool perwave = use_perwave_pass();
+  pa.slot_bytes = perwave ? pass_slot_bytes(pl.NT) : coop_slot_bytes(pl.NT, p);
+  const int approx_prec = opt.hessian_mode == DLSA_HESSIAN_MIXED_F32 ? PREC_F32 : PREC_BF16;
 
   SolveArgs sa;
   memset(&sa, 0, sizeof(sa));
@@ -361,24 +408,58 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
   } hfree{h_cnt};
 
   int it = 0;
-  for (; it < max_iter && (n_running[0] + n_running[1]) > 0 && pl.n_chunks > 0; ++it) {
+  for (size_t lvl = 0; lvl < plans.size(); ++lvl) {
+    const Plan& q = plans[lvl];
+    const bool final_level = lvl + 1 == plans.size();
+    DLSA_HIP_TRY(upload(q));
+    if (lvl > 0) {  // re-enter every running partition
+      DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
+      DLSA_HIP_TRY(launch_level_reset(K, P, start_phase, d_phase, status, d_llprev, d_bt, theta,
+                                      d_cnt, stream));
+      DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, stream));
+      DLSA_HIP_TRY(hipStreamSynchronize(stream));
+      n_running[0] = h_cnt[0];
+      n_running[1] = h_cnt[1];
+    }
+    sa.subsample = final_level ? 0 : 1;
+    sa.level_tol = 1e-2;  // the prefix MLE is only ~sqrt(P/n) from the full one
+    sa.switch_tol = final_level ? opt.switch_tol : 0.0;
+    const int it_end = final_level ? max_iter : std::min(max_iter, it + 10);
+  for (; it < it_end && (n_running[0] + n_running[1]) > 0 && q.n_chunks > 0; ++it) {
     for (int ph = 0; ph < 2; ++ph) {
       if (n_running[ph] == 0) continue;
       const bool f64 = ph == PHASE_F64;
       pa.want_phase = ph;
-      int waves = pass_waves_per_cu(f64);
-      if (const char* e = getenv(f64 ? "DLSA_WAVES_F64" : "DLSA_WAVES_F32")) waves = atoi(e);
-      int nslot = (160 * 1024 / std::max(waves, 1)) / pa.slot_bytes;
-      nslot = std::max(2, std::min(nslot, 4));
-      if (const char* e = getenv("DLSA_NSLOT")) nslot = std::max(2, std::min(atoi(e), 4));
+      int nslot;
+      if (perwave) {
+        int waves = pass_waves_per_cu(f64);
+        if (const char* e = getenv(f64 ? "DLSA_WAVES_F64" : "DLSA_WAVES_F32")) waves = atoi(e);
+        nslot = (160 * 1024 / std::max(waves, 1)) / pa.slot_bytes;
+        nslot = std::max(2, std::min(nslot, 4));
+      } else {
+        // bf16/fp32 passes: one workgroup per CU with a deep ring (HBM-bound);
+        // fp64 passes: two workgroups per CU so one's VALU row phase overlaps
+        // the other's MFMA tile phase (MFMA-bound)
+        int wg_per_cu = (f64 && pl.NT < 8) ? 2 : 1;
+        if (const char* e = getenv(f64 ? "DLSA_WG_F64" : "DLSA_WG_LOWP")) wg_per_cu = atoi(e);
+        const int budget =
+            160 * 1024 / std::max(wg_per_cu, 1) - (2 * kCoopRows + 2 * pl.PP) * 8;
+        nslot = std::max(2, std::min(budget / pa.slot_bytes, 6));
+      }
+      if (const char* e = getenv("DLSA_NSLOT")) nslot = std::max(2, std::min(atoi(e), perwave ? 4 : 6));
       pa.nslot = nslot;
       DLSA_HIP_TRY(timed(f64 ? &g_stats.ms_pass_fp64 : &g_stats.ms_pass_fp32, [&] {
-        return launch_irls_pass(pa, pl.NT, f64, standardize, family, pl.n_chunks, stream);
+        if (perwave)
+          return launch_irls_pass(pa, q.NT, f64, standardize, family, q.n_chunks, stream);
+        return launch_irls_coop(pa, q.NT, f64 ? PREC_F64 : approx_prec, standardize, family,
+                                q.n_chunks, stream);
       }));
       if (f64) {
         g_stats.passes_fp64++;
+        g_stats.rows_fp64 += plan_rows[lvl];
       } else {
         g_stats.passes_fp32++;
+        g_stats.rows_fp32 += plan_rows[lvl];
       }
     }
     DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
@@ -388,10 +469,8 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
     n_running[0] = h_cnt[0];
     n_running[1] = h_cnt[1];
   }
+  }
   g_stats.iterations = it;
-  // rows streamed per pass kind (all chunks are launched; idle ones exit)
-  g_stats.rows_fp32 = (int64_t)g_stats.passes_fp32 * n_total;
-  g_stats.rows_fp64 = (int64_t)g_stats.passes_fp64 * n_total;
 
   DLSA_HIP_TRY(launch_fit_finalize(K, P, theta, sig_inv, sig_inv_theta, status, stream));
   DLSA_HIP_TRY(hipStreamSynchronize(stream));

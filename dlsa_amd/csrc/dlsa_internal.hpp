@@ -13,12 +13,18 @@ namespace dlsa {
 // Per-partition Newton phase.  MIXED fits start in PHASE_F32 (fp32-MFMA
 // Hessian, fp64 gradient) and switch to PHASE_F64 for the pass whose Hessian
 // is returned as Sig_inv; FP64 fits start in PHASE_F64.
-enum : int32_t { PHASE_F32 = 0, PHASE_F64 = 1, PHASE_DONE = 2 };
+// PHASE_LEVEL_DONE: finished the current warm-start subsample level.
+enum : int32_t { PHASE_F32 = 0, PHASE_F64 = 1, PHASE_DONE = 2, PHASE_LEVEL_DONE = 3 };
 enum : int32_t { STATUS_RUNNING = -1 };
 enum : int32_t { FAMILY_LOGISTIC = 0, FAMILY_GAUSSIAN = 1 };
 
 // Rows of X one wave stages per LDS slot (4 MFMA k-steps of 4 rows).
 constexpr int kRowsPerBlock = 8;
+// Cooperative pass: 4 waves per workgroup, 32-row blocks.
+constexpr int kCoopWaves = 4;
+constexpr int kCoopRows = 32;
+// MFMA arithmetic of a pass's Hessian.
+enum : int32_t { PREC_BF16 = 0, PREC_F32 = 1, PREC_F64 = 2 };
 
 // Arguments of the fused IRLS pass (one wave = one chunk of one partition).
 struct PassArgs {
@@ -64,20 +70,28 @@ struct SolveArgs {
   int32_t P;
   int32_t NT;
   int32_t family;  // FAMILY_LOGISTIC: Newton to tol; FAMILY_GAUSSIAN: one exact step
+  int32_t subsample;  // 1 on a warm-start level (row prefix of each partition)
   double tol;
   double switch_tol;
+  double level_tol;   // warm-start level: stop when max|step| <= level_tol (1+max|theta|)
 };
 
 // Launchers (defined in the .hip files).
 hipError_t launch_irls_pass(const PassArgs& a, int NT, bool f64, bool standardize,
                             int family, int n_chunks, hipStream_t s);
 int pass_slot_bytes(int NT);
+hipError_t launch_irls_coop(const PassArgs& a, int NT, int prec, bool standardize, int family,
+                            int n_chunks, hipStream_t s);
+int coop_slot_bytes(int NT, int p);
 int pass_waves_per_cu(bool f64);
 hipError_t launch_newton_solve(const SolveArgs& a, int K, hipStream_t s);
 hipError_t launch_fit_init(const int64_t* offsets_dev, int K, int P, int start_phase,
                            double* theta, int32_t* phase, int32_t* backtracks,
                            int32_t* iters, int32_t* status, double* ll_prev,
                            double* sig_inv, double* loglik, hipStream_t s);
+hipError_t launch_level_reset(int K, int P, int start_phase, int32_t* phase, int32_t* status,
+                              double* ll_prev, int32_t* backtracks, double* theta,
+                              int32_t* counters, hipStream_t s);
 hipError_t launch_fit_finalize(int K, int P, const double* theta, const double* sig_inv,
                                double* sig_inv_theta, int32_t* status, hipStream_t s);
 hipError_t launch_reduce_partitions(const double* sig_inv, const double* sig_inv_theta,

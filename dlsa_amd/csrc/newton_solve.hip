@@ -97,8 +97,20 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
   const int it = a.iters[k];
   double* th = a.theta + (int64_t)k * P;
 
+  // a warm-start level that fails (separation, too few rows) only restarts
+  // the partition from theta = 0 on the next level
+  auto level_fail = [&]() {
+    for (int f = tid; f < P; f += 256) th[f] = 0.0;
+    if (tid == 0) {
+      a.phase[k] = PHASE_LEVEL_DONE;
+      a.iters[k] = it + 1;
+    }
+  };
   if (!isfinite(ll)) {
-    if (tid == 0) a.status[k] = DLSA_STATUS_NONFINITE;
+    if (a.subsample)
+      level_fail();
+    else if (tid == 0)
+      a.status[k] = DLSA_STATUS_NONFINITE;
     return;
   }
 
@@ -122,12 +134,14 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
   }
 
   // 3. publish the information matrix at the evaluation point --------------
-  double* S = a.sig_inv + (int64_t)k * P * P;
-  for (int e = tid; e < P * P; e += 256) {
-    const int i = e / P;
-    S[e] = H[i * LD + (e - i * P)];
+  if (!a.subsample) {
+    double* S = a.sig_inv + (int64_t)k * P * P;
+    for (int e = tid; e < P * P; e += 256) {
+      const int i = e / P;
+      S[e] = H[i * LD + (e - i * P)];
+    }
+    if (tid == 0) a.loglik[k] = ll;
   }
-  if (tid == 0) a.loglik[k] = ll;
   __syncthreads();
 
   // 4. Cholesky, right-looking, lower, in place.  Thread (row = tid/2,
@@ -164,6 +178,10 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
   }
   __syncthreads();
   if (!ok) {
+    if (a.subsample) {
+      level_fail();
+      return;
+    }
     if (tid == 0) {
       if (phase == PHASE_F32 && a.family == FAMILY_LOGISTIC) {
         // fp32 Hessian lost definiteness: redo this point with fp64
@@ -232,6 +250,23 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
       a.iters[k] = it + 1;
       a.status[k] = isfinite(dm) ? DLSA_STATUS_OK : DLSA_STATUS_NONFINITE;
       a.phase[k] = PHASE_DONE;
+    }
+    return;
+  }
+  if (a.subsample) {
+    if (!isfinite(dm)) {
+      level_fail();
+      return;
+    }
+    if (tid == 0) {
+      a.ll_prev[k] = ll;
+      a.backtracks[k] = 0;
+      a.iters[k] = it + 1;
+      if (dm <= a.level_tol * (1.0 + tm)) {
+        a.phase[k] = PHASE_LEVEL_DONE;
+      } else {
+        atomicAdd(&a.counters[phase], 1);
+      }
     }
     return;
   }

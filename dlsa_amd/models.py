@@ -168,9 +168,10 @@ def logistic_model_batched(X, y, offsets, fit_intercept=False, center=None, scal
     models.py:99-101.
 
     X: [n, p] fp64 (torch tensor on the GPU, or array-like, copied once);
-    y: [n] 0/1; offsets: K+1 host ints.  ``hessian`` = "mixed" (fp32-MFMA
-    Hessian until the Newton step is below ``switch_tol``, then an fp64-MFMA
-    pass; the gradient and the returned Sig_inv are always fp64) or "fp64".
+    y: [n] 0/1; offsets: K+1 host ints.  ``hessian`` = "mixed" (bf16-MFMA
+    Hessian until the Newton step is below ``switch_tol``, then fp64-MFMA
+    passes; the gradient and the returned Sig_inv are always fp64),
+    "mixed_f32" (fp32-MFMA approximate Hessian) or "fp64".
     """
     dev = _require_gpu(device)
     Xd = _dev_f64(X, dev)
@@ -202,7 +203,8 @@ def logistic_model_batched(X, y, offsets, fit_intercept=False, center=None, scal
 
     lib = _hip.load()
     opt = _hip.default_options()
-    opt.hessian_mode = {"mixed": _hip.HESSIAN_MIXED, "fp64": _hip.HESSIAN_FP64}[hessian]
+    opt.hessian_mode = {"mixed": _hip.HESSIAN_MIXED, "fp64": _hip.HESSIAN_FP64,
+                        "mixed_f32": _hip.HESSIAN_MIXED_F32}[hessian]
     opt.switch_tol = float(switch_tol)
     opt.record_timing = 1 if record_timing else 0
     opt.rows_per_chunk = int(rows_per_chunk)

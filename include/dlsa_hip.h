@@ -56,12 +56,15 @@ extern "C" {
 #define DLSA_STATUS_EMPTY 3       /* no rows: zero block, like models.py:84-91 */
 #define DLSA_STATUS_NONFINITE 4   /* NaN/Inf in the data or the iterates */
 
-/* Hessian arithmetic of the Newton passes */
-#define DLSA_HESSIAN_MIXED 0  /* fp32 MFMA Hessian until the step is below
-                                 switch_tol, then one fp64 MFMA pass; the
-                                 gradient, the log-likelihood and the returned
-                                 Sig_inv are always fp64 */
-#define DLSA_HESSIAN_FP64 1   /* fp64 MFMA Hessian on every pass */
+/* Hessian arithmetic of the Newton passes.  The gradient, eta, the weights
+ * and the returned log-likelihood and Sig_inv are fp64 in every mode; the
+ * approximate Hessians only steer Newton (the fp64 gradient fixes the
+ * solution). */
+#define DLSA_HESSIAN_MIXED 0      /* bf16 MFMA Hessian until the step is below
+                                     switch_tol, then fp64 MFMA pass(es) */
+#define DLSA_HESSIAN_FP64 1       /* fp64 MFMA Hessian on every pass */
+#define DLSA_HESSIAN_MIXED_F32 2  /* as MIXED with fp32 MFMA approximate passes
+                                     (for ill-conditioned designs) */
 
 #define DLSA_MAX_P_FUSED 128  /* largest P handled by the per-wave fused pass */
 
@@ -73,20 +76,27 @@ typedef struct dlsa_fit_options {
                                pass (<= 0: default 1e-6) */
   void* workspace;          /* device scratch, NULL: allocate per call */
   int64_t workspace_bytes;  /* size of `workspace` */
-  int32_t rows_per_chunk;   /* <= 0: automatic (rows one wave streams) */
-  int32_t reserved[7];
+  int32_t rows_per_chunk;   /* <= 0: automatic (rows one workgroup streams) */
+  int32_t warm_start;       /* 1 (default): the first Newton iterations run on
+                               row prefixes of each partition (1/16, then 1/4
+                               of the rows, never fewer than max(2048, 64 P))
+                               to a 1e-2 step, then on all rows to tol -- the
+                               fixed point is unchanged; 0: all rows from the
+                               start */
+  int32_t reserved[6];
 } dlsa_fit_options;
 
 typedef struct dlsa_fit_stats {
   int32_t iterations;       /* Newton iterations run (max over partitions) */
-  int32_t passes_fp32;      /* fp32-Hessian pass launches */
+  int32_t passes_fp32;      /* approximate-Hessian (bf16/fp32 MFMA) pass launches */
   int32_t passes_fp64;      /* fp64-Hessian pass launches */
   int32_t n_chunks;         /* waves per pass launch */
   double ms_pass_fp32;      /* summed kernel time (record_timing only) */
   double ms_pass_fp64;
   double ms_solve;          /* per-partition Cholesky/Newton update kernels */
   double ms_total;          /* whole call, host wall clock */
-  int64_t rows_fp32;        /* rows streamed by fp32 passes (sum) */
+  int64_t rows_fp32;        /* rows streamed by approximate-Hessian passes (sum
+                               over launches, warm-start levels included) */
   int64_t rows_fp64;        /* rows streamed by fp64 passes (sum) */
 } dlsa_fit_stats;
 
