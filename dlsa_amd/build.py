@@ -18,7 +18,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libdlsa_hip.so")
-SOURCES = ["irls_pass.hip", "irls_coop.hip", "newton_solve.hip", "aux_kernels.hip", "capi.hip", "lars_host.cpp"]
+SOURCES = ["irls_pass.hip", "irls_coop.hip", "eval_pass.hip", "newton_solve.hip", "aux_kernels.hip", "capi.hip", "lars_host.cpp"]
 HEADERS = ["dlsa_internal.hpp", os.path.join("..", "..", "include", "dlsa_hip.h")]
 ARCH = os.environ.get("DLSA_OFFLOAD_ARCH", "gfx950")
 

@@ -532,6 +532,90 @@ int dlsa_logistic_fit_batched(const double* X, const double* y, const int64_t* o
                                       iters, status, nullptr, stream);
 }
 
+int dlsa_logistic_loglik_batched(const double* X, const double* y, const int64_t* offsets,
+                                 int32_t K, int32_t p, int32_t fit_intercept,
+                                 const double* center, const double* scale,
+                                 const double* betas, int32_t n_beta, double* loglik,
+                                 void* stream_) {
+  g_last_error.clear();
+  hipStream_t stream = (hipStream_t)stream_;
+  int rc = check_offsets(offsets, K);
+  if (rc != DLSA_OK) return rc;
+  const int P = p + (fit_intercept ? 1 : 0);
+  if (p < 0 || P < 1 || P > 512 || n_beta < 1 || n_beta > 16 || !betas || !loglik ||
+      (center == nullptr) != (scale == nullptr)) {
+    set_error("dlsa_logistic_loglik_batched: invalid arguments (1 <= P <= 512, 1 <= n_beta <= 16)");
+    return DLSA_E_INVALID;
+  }
+  const int64_t n_total = offsets[K];
+  if (n_total > 0 && (!X || !y)) {
+    set_error("null X or y");
+    return DLSA_E_INVALID;
+  }
+  Plan pl;
+  make_plan(offsets, K, p, fit_intercept, 0, pl);
+  const int nc = std::max(pl.n_chunks, 1);
+  const int64_t bytes = align_up(8LL * nc, 256) + 3 * align_up(4LL * nc, 256) +
+                        align_up(4LL * (K + 1), 256) + align_up(8LL * nc * n_beta, 256);
+  char* ws = nullptr;
+  DLSA_HIP_TRY(hipMallocAsync((void**)&ws, bytes, stream));
+  struct Free {
+    char* p;
+    hipStream_t s;
+    ~Free() {
+      if (p) (void)hipFreeAsync(p, s);
+    }
+  } freer{ws, stream};
+  int64_t o = 0;
+  int64_t* d_row0 = (int64_t*)(ws + o);
+  o += align_up(8LL * nc, 256);
+  int32_t* d_rows = (int32_t*)(ws + o);
+  o += align_up(4LL * nc, 256);
+  int32_t* d_part = (int32_t*)(ws + o);
+  o += align_up(4LL * nc, 256);
+  int32_t* d_pcb = (int32_t*)(ws + o);
+  o += align_up(4LL * (K + 1), 256);
+  double* d_partial = (double*)(ws + o);
+  if (pl.n_chunks > 0) {
+    DLSA_HIP_TRY(hipMemcpyAsync(d_row0, pl.chunk_row0.data(), 8LL * pl.n_chunks,
+                                hipMemcpyHostToDevice, stream));
+    DLSA_HIP_TRY(hipMemcpyAsync(d_rows, pl.chunk_rows.data(), 4LL * pl.n_chunks,
+                                hipMemcpyHostToDevice, stream));
+    DLSA_HIP_TRY(hipMemcpyAsync(d_part, pl.chunk_part.data(), 4LL * pl.n_chunks,
+                                hipMemcpyHostToDevice, stream));
+  }
+  DLSA_HIP_TRY(hipMemcpyAsync(d_pcb, pl.part_chunk_begin.data(), 4LL * (K + 1),
+                              hipMemcpyHostToDevice, stream));
+  if (pl.n_chunks > 0) {
+    EvalArgs ea;
+    memset(&ea, 0, sizeof(ea));
+    ea.X = X;
+    ea.y = y;
+    ea.chunk_row0 = d_row0;
+    ea.chunk_rows = d_rows;
+    ea.chunk_part = d_part;
+    ea.center = center;
+    ea.scale = scale;
+    ea.betas = betas;
+    ea.partial = d_partial;
+    const uintptr_t xend = (uintptr_t)(X + n_total * (int64_t)p);
+    ea.x_last16 = ((xend + 15) & ~(uintptr_t)15) - 16;
+    ea.y_last4 = (uintptr_t)(y + n_total) - 4;
+    ea.p = p;
+    ea.P = P;
+    ea.intercept = fit_intercept ? 1 : 0;
+    ea.nbeta = n_beta;
+    ea.slot_bytes = eval_slot_bytes(p);
+    const int PM = ((P + 7) / 8) * 8;
+    const int budget = 160 * 1024 - (n_beta * PM + 2 * PM + 64) * 8;
+    ea.nslot = std::max(2, std::min(budget / ea.slot_bytes, 6));
+    DLSA_HIP_TRY(launch_loglik_eval(ea, pl.n_chunks, stream));
+  }
+  DLSA_HIP_TRY(launch_loglik_reduce(d_partial, d_pcb, K, n_beta, loglik, stream));
+  DLSA_HIP_TRY(hipStreamSynchronize(stream));
+  return DLSA_OK;
+}
+
 int dlsa_reduce_partitions(const double* sig_inv, const double* sig_inv_theta,
                            const double* theta, int32_t K, int32_t p, double* out,
                            void* stream) {

@@ -76,7 +76,28 @@ struct SolveArgs {
   double level_tol;   // warm-start level: stop when max|step| <= level_tol (1+max|theta|)
 };
 
+// Arguments of the log-likelihood evaluation pass.
+struct EvalArgs {
+  const double* X;
+  const double* y;
+  const int64_t* chunk_row0;
+  const int32_t* chunk_rows;
+  const int32_t* chunk_part;
+  const double* center;  // [p] or null
+  const double* scale;
+  const double* betas;   // [nbeta, P]
+  double* partial;       // [n_chunks, nbeta]
+  uintptr_t x_last16;
+  uintptr_t y_last4;
+  int32_t p, P, intercept, nbeta;
+  int32_t nslot, slot_bytes;
+};
+
 // Launchers (defined in the .hip files).
+hipError_t launch_loglik_eval(const EvalArgs& a, int n_chunks, hipStream_t s);
+hipError_t launch_loglik_reduce(const double* partial, const int32_t* pcb, int K, int B,
+                                double* out, hipStream_t s);
+int eval_slot_bytes(int p);
 hipError_t launch_irls_pass(const PassArgs& a, int NT, bool f64, bool standardize,
                             int family, int n_chunks, hipStream_t s);
 int pass_slot_bytes(int NT);

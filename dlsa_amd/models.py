@@ -267,6 +267,39 @@ def ols_model_batched(X, y, offsets, fit_intercept=False, center=None, scale=Non
                       _hip.last_fit_stats())
 
 
+def logistic_loglik_batched(X, y, offsets, betas, fit_intercept=False, center=None, scale=None,
+                            device=None):
+    """Per-partition log-likelihood of candidate coefficient vectors in one
+    pass over X (the evaluation step of dlsa/models.py:151-225 /
+    dlsa/model_eval.py:10-42).  betas: [B, P] (B <= 16), intercept first.
+    Returns a [K, B] fp64 tensor on the device."""
+    dev = _require_gpu(device)
+    Xd = _dev_f64(X, dev)
+    yd = _dev_f64(y, dev).reshape(-1)
+    n, p = Xd.shape
+    offs = np.ascontiguousarray(np.asarray(offsets, dtype=np.int64))
+    K = offs.size - 1
+    if K < 1 or offs[0] != 0 or offs[-1] != n or np.any(np.diff(offs) < 0) or yd.numel() != n:
+        raise ValueError("offsets must be non-decreasing, start at 0 and end at n; y has n rows")
+    bd = _dev_f64(betas, dev)
+    if bd.dim() == 1:
+        bd = bd.reshape(1, -1)
+    B, P = bd.shape
+    if P != p + (1 if fit_intercept else 0):
+        raise ValueError("betas must have P = p + fit_intercept columns")
+    cd = sd = None
+    if center is not None or scale is not None:
+        cd = _dev_f64(center, dev).reshape(-1)
+        sd = _dev_f64(scale, dev).reshape(-1)
+    out = torch.empty((K, B), dtype=torch.float64, device=dev)
+    lib = _hip.load()
+    rc = lib.dlsa_logistic_loglik_batched(_ptr(Xd), _ptr(yd), offs.ctypes.data_as(ctypes.c_void_p),
+                                          K, p, int(bool(fit_intercept)), _ptr(cd), _ptr(sd),
+                                          _ptr(bd), B, _ptr(out), _stream(dev))
+    _hip.check(rc, "dlsa_logistic_loglik_batched")
+    return out
+
+
 # ---------------------------------------------------------------------------
 # reference-signature wrapper (one Spark group)
 # ---------------------------------------------------------------------------
@@ -345,3 +378,34 @@ def logistic_model(sample_df, Y_name, fit_intercept=False, dummy_info=[], dummy_
     if out.isna().values.any():
         warnings.warn("NAs appear in the final output")
     return out
+
+
+def logistic_model_eval(sample_df, Y_name, par, fit_intercept=False, dummy_info=[],
+                        dummy_factors_baseline=[], data_info=[]):
+    """Log-likelihood of each coefficient column of ``par`` on one partition
+    (dlsa/models.py:151-225).  ``par`` is a P-row DataFrame (one column per
+    method, e.g. beta_byAIC / beta_byBIC / beta_byOLS / beta_byONESHOT).
+    Returns a one-row DataFrame with the same columns.  A partition missing a
+    dummy level is evaluated with that dummy column set to 0, as the
+    reference does (models.py:185-193).  The pass runs on the GPU."""
+    import pandas as pd
+
+    x_train, numeric, cols, missing = _design(sample_df, Y_name, dummy_info, dummy_factors_baseline)
+    if missing:
+        warnings.warn("Dummies:" + str(set(cols) - set(x_train.columns))
+                      + "missing in this data chunk " + str(x_train.shape))
+    x_train = x_train.reindex(columns=cols, fill_value=0)
+    X = np.ascontiguousarray(x_train.to_numpy(dtype=np.float64))
+    y = np.asarray(sample_df[Y_name], dtype=np.float64)
+    center = scale = None
+    if len(data_info) > 0:
+        center = np.zeros(len(cols))
+        scale = np.ones(len(cols))
+        for j, c in enumerate(cols):
+            if c in numeric:
+                center[j] = _describe_row(data_info, c, 1)
+                scale[j] = _describe_row(data_info, c, 2)
+    betas = np.ascontiguousarray(np.asarray(par, dtype=np.float64).T)
+    ll = logistic_loglik_batched(X, y, np.array([0, X.shape[0]]), betas,
+                                 fit_intercept=fit_intercept, center=center, scale=scale)
+    return pd.DataFrame(ll.cpu().numpy(), columns=list(par.columns))

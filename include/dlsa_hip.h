@@ -164,6 +164,21 @@ int dlsa_ols_fit_batched(const double* X, const double* y, const int64_t* offset
                          int32_t* status, const dlsa_fit_options* opt,
                          void* stream);
 
+/*
+ * Log-likelihood evaluation pass -- replaces the per-partition body of
+ * dlsa/models.py:151-225 logistic_model_eval (driven by dlsa/model_eval.py:
+ * 10-42): for every partition k and candidate vector b (intercept first when
+ * fit_intercept, standardised like the fit),
+ *   loglik[k * n_beta + b] = sum_i y_i x_i.beta_b - log(1 + exp(x_i.beta_b)).
+ * betas [n_beta, P] device, 1 <= n_beta <= 16, P <= 512; loglik [K, n_beta]
+ * device.  One pass over X for all candidates; synchronises the stream.
+ */
+int dlsa_logistic_loglik_batched(const double* X, const double* y,
+                                 const int64_t* offsets, int32_t K, int32_t p,
+                                 int32_t fit_intercept, const double* center,
+                                 const double* scale, const double* betas,
+                                 int32_t n_beta, double* loglik, void* stream);
+
 /* Timing/iteration record of the calling thread's last fit. */
 int dlsa_last_fit_stats(dlsa_fit_stats* out);
 

@@ -27,4 +27,5 @@ from .dlsa_oracle import (  # noqa: F401
     lars_lsa,
     dlsa,
     ols_fit,
+    logistic_loglik,
 )

@@ -200,6 +200,22 @@ def logistic_fit_partitions(X, y, offsets, **kw):
             np.array([o["iters"] for o in outs]))
 
 
+def logistic_loglik(X, y, betas, fit_intercept=False, center=None, scale=None):
+    """Restates the likelihood loop of ``logistic_model_eval``
+    (dlsa/models.py:196-225): for each candidate column beta,
+    sum(y log p + (1 - y) log(1 - p)), p = sigmoid(x . beta), after the same
+    standardisation / intercept handling as the fit (models.py:195-205),
+    evaluated in the stable form y eta - softplus(eta)."""
+    X = np.asarray(X, dtype=np.float64)
+    if center is not None:
+        X = (X - np.asarray(center, np.float64)) / np.asarray(scale, np.float64)
+    if fit_intercept:
+        X = np.concatenate([np.ones((X.shape[0], 1)), X], axis=1)
+    y = np.asarray(y, np.float64).reshape(-1)
+    betas = np.atleast_2d(np.asarray(betas, np.float64))
+    return np.array([_loglik(X @ b, y) for b in betas])
+
+
 def ols_fit(X, y, fit_intercept=False):
     """Closed-form OLS local fit for the linear DLSA path (SURVEY 8(d) config
     4; the reference only has a statsmodels demo,

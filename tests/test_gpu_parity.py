@@ -253,3 +253,41 @@ def test_ols_vs_oracle(torch_cuda, M, p, fi):
             Xk = np.column_stack([np.ones(len(Xk)), Xk])
         rss = float(((y[off[k]:off[k + 1]] - Xk @ o["coef"]) ** 2).sum())
         assert abs(fit.loglik[k].item() - rss) < 1e-6 * rss
+
+
+@pytest.mark.parametrize("p,fi,std", [(10, False, False), (100, True, False), (37, True, True)])
+def test_loglik_eval_vs_oracle(torch_cuda, M, p, fi, std):
+    """Evaluation pass (models.py:151-225): per-partition log-likelihood of 4
+    candidate vectors (AIC / BIC / WLSE / ONESHOT in the reference driver)."""
+    rs = np.random.RandomState(p)
+    sizes = [5000, 3001, 777]
+    n = sum(sizes)
+    X, y = O.simulate_counter(n, p, seed=3 * p)
+    if std:
+        X = X * 3.0 + 1.5
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    P = p + fi
+    betas = rs.randn(4, P) * 0.5
+    center = X.mean(0) if std else None
+    scale = X.std(0) if std else None
+    ll = M.logistic_loglik_batched(X, y, off, betas, fit_intercept=fi, center=center,
+                                   scale=scale).cpu().numpy()
+    for k in range(3):
+        ref = O.logistic_loglik(X[off[k]:off[k + 1]], y[off[k]:off[k + 1]], betas,
+                                fit_intercept=fi, center=center, scale=scale)
+        assert np.abs(ll[k] - ref).max() <= 1e-10 * np.abs(ref).max()
+
+
+def test_logistic_model_eval_reference_signature(torch_cuda, M):
+    import pandas as pd
+
+    p = 6
+    X, y = O.simulate_counter(4000, p, seed=17)
+    df = pd.DataFrame(np.column_stack([np.zeros(4000), y, X]),
+                      columns=["partition_id", "label"] + [f"x{i}" for i in range(p)])
+    par = pd.DataFrame(np.random.RandomState(1).randn(p + 1, 4),
+                       columns=["beta_byAIC", "beta_byBIC", "beta_byOLS", "beta_byONESHOT"])
+    out = M.logistic_model_eval(df, "label", par, fit_intercept=True)
+    ref = O.logistic_loglik(X, y, par.to_numpy().T, fit_intercept=True)
+    assert list(out.columns) == list(par.columns)
+    assert np.abs(out.to_numpy()[0] - ref).max() <= 1e-10 * np.abs(ref).max()
