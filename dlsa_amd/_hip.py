@@ -21,7 +21,7 @@ STATUS_NAMES = {0: "ok", 1: "maxiter", 2: "singular", 3: "empty", 4: "nonfinite"
 HESSIAN_MIXED = 0
 HESSIAN_FP64 = 1
 HESSIAN_MIXED_F32 = 2
-MAX_P_FUSED = 128
+MAX_P_FUSED = 192
 
 
 class DlsaHipError(RuntimeError):

@@ -18,8 +18,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libdlsa_hip.so")
-SOURCES = ["irls_pass.hip", "irls_coop.hip", "eval_pass.hip", "newton_solve.hip", "aux_kernels.hip", "capi.hip", "lars_host.cpp"]
-HEADERS = ["dlsa_internal.hpp", os.path.join("..", "..", "include", "dlsa_hip.h")]
+SOURCES = (["irls_pass.hip", "irls_coop.hip"] + [f"irls_coop_g{i}.hip" for i in range(1, 7)] +
+           ["eval_pass.hip", "newton_solve.hip", "aux_kernels.hip", "capi.hip", "lars_host.cpp"])
+HEADERS = ["dlsa_internal.hpp", "irls_coop_impl.hpp", os.path.join("..", "..", "include", "dlsa_hip.h")]
 ARCH = os.environ.get("DLSA_OFFLOAD_ARCH", "gfx950")
 
 
@@ -39,18 +40,38 @@ def _stale() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()) -> str:
+    """Compile every source to an object in parallel, then link the .so."""
     if not force and out == OUT and not _stale():
         return OUT
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", "-Wno-unused-command-line-argument",
-           "-I" + os.path.join(ROOT, "include"), *[f"-D{d}" for d in defines],
-           *[os.path.join(CSRC, s) for s in SOURCES], "-o", out + ".tmp"]
-    if verbose:
-        print(" ".join(cmd), flush=True)
-    res = subprocess.run(cmd, capture_output=True, text=True)
-    if res.returncode != 0:
-        sys.stderr.write(res.stdout + res.stderr)
-        raise RuntimeError(f"hipcc failed ({res.returncode})")
+    import tempfile
+    from concurrent.futures import ThreadPoolExecutor
+
+    common = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
+              "-Wall", "-Wno-unused-function", "-Wno-unused-command-line-argument",
+              "-I" + os.path.join(ROOT, "include"), *[f"-D{d}" for d in defines]]
+    jobs = int(os.environ.get("DLSA_BUILD_JOBS", min(8, os.cpu_count() or 1)))
+    with tempfile.TemporaryDirectory(prefix="dlsa_build_") as tmp:
+        def compile_one(src):
+            obj = os.path.join(tmp, os.path.splitext(src)[0] + ".o")
+            cmd = common + ["-c", os.path.join(CSRC, src), "-o", obj]
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            return obj, subprocess.run(cmd, capture_output=True, text=True)
+
+        with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+            results = list(ex.map(compile_one, SOURCES))
+        for obj, res in results:
+            if res.returncode != 0:
+                sys.stderr.write(res.stdout + res.stderr)
+                raise RuntimeError(f"hipcc failed on {obj} ({res.returncode})")
+        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC",
+               *[o for o, _ in results], "-o", out + ".tmp"]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode != 0:
+            sys.stderr.write(res.stdout + res.stderr)
+            raise RuntimeError(f"link failed ({res.returncode})")
     os.replace(out + ".tmp", out)
     return out
 

@@ -46,6 +46,7 @@ static bool use_perwave_pass() {
 }
 
 static int auto_rows_per_chunk(int64_t n_total) {
+  if (const char* e = getenv("DLSA_ROWS_PER_CHUNK")) return std::max(64, atoi(e));
   if (use_perwave_pass()) {
     // one wave per chunk: ~8 waves per CU-slot round on 256 CUs
     int64_t r = n_total / 4096;
@@ -343,6 +344,10 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
   pa.P = P;
   pa.intercept = fit_intercept ? 1 : 0;
   const bool perwave = use_perwave_pass();
+  if (perwave && pl.NT > 8) {
+    set_error("DLSA_PASS=perwave handles P <= 128 only");
+    return DLSA_E_UNSUPPORTED;
+  }
   pa.slot_bytes = perwave ? pass_slot_bytes(pl.NT) : coop_slot_bytes(pl.NT, p);
   const int approx_prec = opt.hessian_mode == DLSA_HESSIAN_MIXED_F32 ? PREC_F32 : PREC_BF16;
 
@@ -443,7 +448,7 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
         int wg_per_cu = (f64 && pl.NT < 8) ? 2 : 1;
         if (const char* e = getenv(f64 ? "DLSA_WG_F64" : "DLSA_WG_LOWP")) wg_per_cu = atoi(e);
         const int budget =
-            160 * 1024 / std::max(wg_per_cu, 1) - (2 * kCoopRows + 2 * pl.PP) * 8;
+            160 * 1024 / std::max(wg_per_cu, 1) - coop_extra_bytes(pl.NT);
         nslot = std::max(2, std::min(budget / pa.slot_bytes, 6));
       }
       if (const char* e = getenv("DLSA_NSLOT")) nslot = std::max(2, std::min(atoi(e), perwave ? 4 : 6));

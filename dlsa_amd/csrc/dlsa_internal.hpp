@@ -104,6 +104,7 @@ int pass_slot_bytes(int NT);
 hipError_t launch_irls_coop(const PassArgs& a, int NT, int prec, bool standardize, int family,
                             int n_chunks, hipStream_t s);
 int coop_slot_bytes(int NT, int p);
+int coop_extra_bytes(int NT);  // LDS beyond the ring
 int pass_waves_per_cu(bool f64);
 hipError_t launch_newton_solve(const SolveArgs& a, int K, hipStream_t s);
 hipError_t launch_fit_init(const int64_t* offsets_dev, int K, int P, int start_phase,

@@ -1,0 +1,15 @@
+// Instantiations of the cooperative pass for NT in {11, 12}.
+#include "irls_coop_impl.hpp"
+
+namespace dlsa {
+
+hipError_t launch_irls_coop_g6(const PassArgs& a, int NT, int prec, bool std_, int family,
+                                int n_chunks, hipStream_t s) {
+  switch (NT) {
+    case 11: return launch_coop_nt<11>(a, prec, std_, family, n_chunks, s);
+    case 12: return launch_coop_nt<12>(a, prec, std_, family, n_chunks, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace dlsa

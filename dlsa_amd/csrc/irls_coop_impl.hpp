@@ -1,0 +1,489 @@
+// Cooperative fused IRLS pass (gfx950 / CDNA4) -- kernel templates, included
+// by the irls_coop*.hip translation units (one per group of NT values, so the
+// instantiations compile in parallel).
+//
+// Cooperative fused IRLS pass: one 4-wave workgroup streams
+// a chunk of rows of one partition through a shared LDS-DMA ring.
+//
+// Replaces, per Newton iteration, the per-partition work of the reference map
+// stage (sklearn newton-cg Hessian-vector passes, predict_proba and
+// Sig_inv = X^T diag(p(1-p)) X, dlsa/models.py:110-131) with ONE pass over X.
+//
+// Per 32-row block:
+//   B1  barrier: the block's DMA pieces (issued by all 4 waves, each waiting
+//       on its own counted vmcnt) have landed; the slot of block b-1 is free
+//       and receives block b+S-1 (S-1 blocks always in flight).
+//   B   row phase: rows split over the waves, 8 lanes per row.  eta = x.theta
+//       (fp64, 8-lane DPP reduction), mu, w = mu(1-mu), r = y - mu, the
+//       gradient x*r and the log-likelihood are computed ONCE per row; w and r
+//       are published in LDS.
+//   B2  barrier.
+//   C   tile phase: the lower-triangle 16x16 tiles of X^T W X are split over
+//       the waves (contiguous tile ranges, so each wave touches few column
+//       tiles).  PREC_BF16: one v_mfma_f32_16x16x32_bf16 per tile per block;
+//       PREC_F32 / PREC_F64: 8 k-steps of v_mfma_*_16x16x4 (fp32 / fp64).
+// The bf16 / fp32 Hessians only steer Newton (the fp64 gradient fixes the
+// fixed point); the returned Sig_inv always comes from a PREC_F64 pass.
+#include <stdlib.h>
+
+#include <type_traits>
+#include <utility>
+
+#pragma once
+
+#include "dlsa_internal.hpp"
+
+namespace dlsa {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef const __attribute__((address_space(1))) void gbl_void_t;
+
+namespace {
+
+constexpr int RB = kCoopRows;   // rows per block
+
+// Profiling-only ablations (tools/build_variants.sh builds them into separate
+// .so files; the product build has DLSA_ABLATE = 0): 1 no tile phase, 2 no
+// transcendentals in the row phase, 3 stream only, 4 no row phase.
+#ifndef DLSA_ABLATE
+#define DLSA_ABLATE 0
+#endif
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits on gfx950");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vmcnt_le(int n) {
+  if constexpr (N <= 0) {
+    wait_vmcnt<0>();
+  } else {
+    if (n >= N)
+      wait_vmcnt<N>();
+    else
+      wait_vmcnt_le<N - 1>(n);
+  }
+}
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+// Sum over the LPR (8 or 16) lanes of a row group.  8: quad xor1, quad xor2,
+// half-row mirror; 16: row_ror 8, 4, 2, 1.  Every lane ends with the
+// bitwise-identical total (each step adds a commutative pair).
+template <int LPR>
+__device__ __forceinline__ double red_row(double v) {
+  if constexpr (LPR == 8) {
+    v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+    v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+    v += dpp_f64<0x141>(v);  // row_half_mirror
+  } else {
+    static_assert(LPR == 16, "8 or 16 lanes per row");
+    v += dpp_f64<0x128>(v);
+    v += dpp_f64<0x124>(v);
+    v += dpp_f64<0x122>(v);
+    v += dpp_f64<0x121>(v);
+  }
+  return v;
+}
+
+constexpr int tile_I(int t) {
+  int I = 0;
+  while ((I + 1) * (I + 2) / 2 <= t) ++I;
+  return I;
+}
+constexpr int tile_J(int t) { return t - tile_I(t) * (tile_I(t) + 1) / 2; }
+
+template <int NT, int W_>
+struct CG {
+  static constexpr int W = W_;                // waves per workgroup (4 or 8)
+  static constexpr int RPW = RB / W;          // rows per wave in the row phase
+  static constexpr int LPR = 64 / RPW;        // lanes per row in the row phase (8 or 16)
+  static constexpr int PMAX = 16 * NT;
+  static constexpr int T = NT * (NT + 1) / 2;
+  static constexpr int TPW = (T + W - 1) / W;  // tiles per wave (contiguous ranges)
+  static constexpr int M = PMAX / LPR;         // features per lane in the row phase
+  static constexpr int PAD = 16;
+  static constexpr int MAX_PIECES = (RB * PMAX * 8 + 16 + 1023) / 1024;
+  static constexpr int MAX_D = (MAX_PIECES + W - 1) / W;  // DMA pieces per wave per block
+  // tiles of wave `wid`: t in [wid*TPW, min(T, (wid+1)*TPW))
+  static constexpr unsigned col_mask(int wid) {
+    unsigned m = 0;
+    for (int t = wid * TPW; t < T && t < (wid + 1) * TPW; ++t)
+      m |= (1u << tile_I(t)) | (1u << tile_J(t));
+    return m;
+  }
+  static constexpr unsigned row_mask(int wid) {
+    unsigned m = 0;
+    for (int t = wid * TPW; t < T && t < (wid + 1) * TPW; ++t) m |= 1u << tile_I(t);
+    return m;
+  }
+};
+
+template <typename F, int... Is>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, Is...>) {
+  (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+__host__ __device__ __forceinline__ int npieces_for(int p) { return (RB * p * 8 + 16 + 1023) / 1024; }
+
+}  // namespace
+
+// Waves per workgroup: 4 for P <= 128 (8 lanes per row in the row phase),
+// 8 above (16 lanes per row keeps the per-lane feature count <= 12).
+// DLSA_COOP_W=8 selects 8 waves for small P too (profiling knob).
+inline int coop_waves(int NT) {
+  if (NT > 8) return 8;
+  if (const char* e = getenv("DLSA_COOP_W")) return atoi(e) == 8 ? 8 : 4;
+  return 4;
+}
+
+inline int coop_slot_bytes_impl(int NT, int p) {
+  const int W = coop_waves(NT);
+  const int npieces = npieces_for(p);
+  const int d = (npieces + W - 1) / W;
+  return 16 + d * W * 1024 + 16 * NT * 8 + RB * 8;
+}
+
+// LDS beyond the ring: w, r of the block [2][RB] fp64, center / 1/scale
+// [2][PMAX] fp64, and the bf16 MFMA operands of the block: x and w*x,
+// [PMAX][RB] bf16 each (feature-major, so one lane's 8 consecutive k are one
+// 16-byte read).
+inline int coop_extra_bytes_impl(int NT) {
+  return (2 * RB + 2 * 16 * NT) * 8 + 2 * 16 * NT * RB * 2;
+}
+
+// Tile phase of wave WID for one 32-row block.
+template <int NT, int W, int PREC, bool STD, int WID, typename Acc>
+__device__ __forceinline__ void tile_phase(Acc (&acc)[(CG<NT, W>::TPW)], const double* xs,
+                                           const double* wr, int p, int ic, int lane,
+                                           const double* stdv, const __bf16* obx) {
+  using G = CG<NT, W>;
+  constexpr unsigned CM = G::col_mask(WID);
+  constexpr unsigned RM = G::row_mask(WID);
+  const int fl = lane & 15, q = lane >> 4;
+  const bool icpt_lane = ic && fl == 0;
+  const double* xq = xs + q * p + (fl - ic);  // row q of the block, this lane's feature
+  if constexpr (PREC == PREC_BF16) {
+    // operands staged by the row phase: k index 8q + j = block row 8q + j
+    const __bf16* obw = obx + G::PMAX * RB;
+    bf16x8 Bv[NT], Av[NT];
+    static_for<NT>([&](auto cI) {
+      constexpr int c = decltype(cI)::value;
+      if constexpr ((CM >> c) & 1u) {
+        const int o = (16 * c + fl) * RB + 8 * q;
+        Bv[c] = *(const bf16x8*)(obx + o);
+        if constexpr ((RM >> c) & 1u) Av[c] = *(const bf16x8*)(obw + o);
+      }
+    });
+    static_for<G::TPW>([&](auto iI) {
+      constexpr int i = decltype(iI)::value;
+      constexpr int t = WID * G::TPW + i;
+      if constexpr (t < G::T) {
+        constexpr int I = tile_I(t), J = tile_J(t);
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Av[I], Bv[J], acc[i], 0, 0, 0);
+      }
+    });
+  } else {
+    // 8 k-steps of 4 rows: k-step s uses block rows 4s + q (k = q)
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const double ws = wr[4 * s + q];
+      double xv[NT], av[NT];
+      static_for<NT>([&](auto cI) {
+        constexpr int c = decltype(cI)::value;
+        if constexpr ((CM >> c) & 1u) {
+          double v = xq[4 * s * p + 16 * c];
+          if constexpr (STD) v = (v - stdv[16 * c + fl]) * stdv[G::PMAX + 16 * c + fl];
+          if (c == 0 && icpt_lane) v = 1.0;
+          xv[c] = v;
+          if constexpr ((RM >> c) & 1u) av[c] = v * ws;
+        }
+      });
+      static_for<G::TPW>([&](auto iI) {
+        constexpr int i = decltype(iI)::value;
+        constexpr int t = WID * G::TPW + i;
+        if constexpr (t < G::T) {
+          constexpr int I = tile_I(t), J = tile_J(t);
+          if constexpr (PREC == PREC_F64)
+            acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[I], xv[J], acc[i], 0, 0, 0);
+          else
+            acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32((float)av[I], (float)xv[J], acc[i], 0,
+                                                          0, 0);
+        }
+      });
+    }
+  }
+}
+
+template <int NT, int W, int PREC, bool STD, int WID, typename Acc>
+__device__ __forceinline__ void store_tiles(Acc (&acc)[(CG<NT, W>::TPW)], double* sH, int lane) {
+  using G = CG<NT, W>;
+  const int fl = lane & 15, q = lane >> 4;
+  static_for<G::TPW>([&](auto iI) {
+    constexpr int i = decltype(iI)::value;
+    constexpr int t = WID * G::TPW + i;
+    if constexpr (t < G::T) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        // f64 16x16x4 C/D map: row = (l>>4) + 4*reg; f32 16x16 maps: 4*(l>>4) + reg
+        const int row = (PREC == PREC_F64) ? (q + 4 * r) : (4 * q + r);
+        sH[t * 256 + row * 16 + fl] = (double)acc[i][r];
+      }
+    }
+  });
+}
+
+template <int NT, int W, int PREC, bool STD, int FAM>
+__global__ __launch_bounds__(64 * W, (W == 8 || (PREC == PREC_F64 && NT < 8)) ? 2 : 1)
+void irls_coop_kernel(const PassArgs a) {
+  using G = CG<NT, W>;
+  using Acc = typename std::conditional<PREC == PREC_F64, d4, f4>::type;
+  constexpr int RPW = G::RPW, LPR = G::LPR;
+  constexpr int M = G::M;
+  constexpr int MAXW = 4 * (G::MAX_D + 1);  // nslot <= 6
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int chunk = blockIdx.x;
+  const int part = a.chunk_part[chunk];
+  if (a.phase[part] != a.want_phase) return;  // workgroup-uniform
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int p = a.p, P = a.P, ic = a.intercept;
+  const int64_t row0 = a.chunk_row0[chunk];
+  const int nrows = a.chunk_rows[chunk];
+  const int nb = (nrows + RB - 1) / RB;
+  const int nslot = a.nslot;
+  const int slot_bytes = a.slot_bytes;
+  const int npieces = npieces_for(p);
+  const int d = (npieces + W - 1) / W;
+  const int slot_x = G::PAD + d * W * 1024 + G::PMAX * 8;  // y follows
+  double* wr = (double*)(smem + nslot * slot_bytes);       // [2][RB]: w, r of the block
+  double* stdv = wr + 2 * RB;  // [2][PMAX]: center, 1/scale by feature (STD only)
+  __bf16* obx = (__bf16*)(stdv + 2 * G::PMAX);  // [2][PMAX][RB] bf16 operands (PREC_BF16)
+
+  // ---- row-phase constants: lane handles features f = sl + 8m ------------
+  const int sl = lane % LPR;
+  const int rB = wid * RPW + lane / LPR;  // block row of this lane in the row phase
+  double beta[M], gacc[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const int f = sl + LPR * m;
+    beta[m] = (f < P) ? a.theta[(int64_t)part * P + f] : 0.0;
+    gacc[m] = 0.0;
+  }
+  double llacc = 0.0;
+  Acc acc[G::TPW];
+#pragma unroll
+  for (int i = 0; i < G::TPW; ++i) acc[i] = Acc{0, 0, 0, 0};
+
+  // zero the ring once: pads/tails and never-DMA'd bytes must be finite
+  for (int o = tid * 16; o < nslot * slot_bytes; o += 64 * W * 16)
+    *(uint4*)(smem + o) = make_uint4(0, 0, 0, 0);
+  if constexpr (STD) {
+    for (int f = tid; f < G::PMAX; f += 64 * W) {
+      const int j = f - ic;
+      const bool in = j >= 0 && j < p;
+      stdv[f] = in ? a.center[j] : 0.0;
+      stdv[G::PMAX + f] = in ? 1.0 / a.scale[j] : 1.0;
+    }
+  }
+  __syncthreads();
+
+  auto issue = [&](int blk) {
+    const int bb = blk < nb ? blk : nb - 1;  // tail: harmless re-fetch, fixed counts
+    char* sbase = smem + (blk % nslot) * slot_bytes;
+    const uintptr_t start = (uintptr_t)(a.X + (row0 + (int64_t)bb * RB) * p);
+    const uintptr_t al = start & ~(uintptr_t)15;
+    for (int i = 0; i < d; ++i) {
+      int j = wid + W * i;
+      const int jj = j < npieces ? j : npieces - 1;
+      uintptr_t src = al + (uintptr_t)jj * 1024 + (uintptr_t)lane * 16;
+      src = src < a.x_last16 ? src : a.x_last16;
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)src,
+                                       (lds_void_t*)(sbase + G::PAD + j * 1024), 16, 0, 0);
+    }
+    uintptr_t ys = (uintptr_t)(a.y + row0 + (int64_t)bb * RB) + (uintptr_t)lane * 4;
+    ys = ys < a.y_last4 ? ys : a.y_last4;
+    __builtin_amdgcn_global_load_lds((gbl_void_t*)ys, (lds_void_t*)(sbase + slot_x), 4, 0, 0);
+  };
+
+  for (int b = 0; b < nslot - 1; ++b) issue(b);
+  const int keep = (nslot - 2) * (d + 1);
+
+  for (int b = 0; b < nb; ++b) {
+    wait_vmcnt_le<MAXW>(keep);  // this wave's pieces of block b landed
+    __syncthreads();            // B1: everyone's pieces landed, block b-1 fully consumed
+    issue(b + nslot - 1);
+
+    const char* slot = smem + (b % nslot) * slot_bytes;
+    const uintptr_t start = (uintptr_t)(a.X + (row0 + (int64_t)b * RB) * p);
+    const double* xs = (const double*)(slot + G::PAD + (start & 15));
+    const double* ys = (const double*)(slot + slot_x);
+    const int rows_left = nrows - b * RB;
+
+    // ---- B: row phase ------------------------------------------------------
+    if constexpr (DLSA_ABLATE != 3 && DLSA_ABLATE != 4) {
+      const bool valid = rB < rows_left;
+      const double* xr = xs + rB * p + (sl - ic);
+      double xv[M];
+      double e = 0.0;
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        double v = xr[LPR * m];
+        if constexpr (STD) v = (v - stdv[sl + LPR * m]) * stdv[G::PMAX + sl + LPR * m];
+        if (m == 0 && ic && sl == 0) v = 1.0;
+        xv[m] = v;
+        e = fma(v, beta[m], e);
+      }
+      e = red_row<LPR>(e);
+      const double yv = ys[rB];
+      double w, r;
+      if constexpr (FAM == FAMILY_LOGISTIC && DLSA_ABLATE == 2) {
+        w = 0.25;
+        r = yv - 0.5 - 0.25 * e;
+        if (valid && sl == 0) llacc += e;
+      } else if constexpr (FAM == FAMILY_LOGISTIC) {
+        const double ea = exp(-fabs(e));
+        const double inv = 1.0 / (1.0 + ea);
+        const double mu = e >= 0.0 ? inv : ea * inv;
+        w = ea * inv * inv;  // mu (1 - mu), cancellation free
+        r = yv - mu;
+        if (valid && sl == 0) {
+          // exact fp64 in the fp64 pass (its value is returned); fp32 log in
+          // the approximate passes, where it only drives step halving
+          const double sp = (PREC == PREC_F64) ? log1p(ea) : (double)__logf(1.0f + (float)ea);
+          llacc += yv * e - (fmax(e, 0.0) + sp);
+        }
+      } else {  // gaussian (OLS): mu = eta, w = 1, ll = -rss/2
+        w = 1.0;
+        r = yv - e;
+        if (valid && sl == 0) llacc -= 0.5 * r * r;
+      }
+      if (!valid) {
+        w = 0.0;
+        r = 0.0;
+      }
+#pragma unroll
+      for (int m = 0; m < M; ++m) gacc[m] = fma(xv[m], r, gacc[m]);
+      if (sl == 0) {
+        wr[rB] = w;
+        wr[RB + rB] = r;
+      }
+      if constexpr (PREC == PREC_BF16) {
+        // stage the bf16 MFMA operands once per row (x and w*x)
+        const float wf = (float)w;
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+          const int o = (sl + LPR * m) * RB + rB;
+          const float xf = (float)xv[m];
+          obx[o] = (__bf16)xf;
+          obx[G::PMAX * RB + o] = (__bf16)(xf * wf);
+        }
+      }
+    }
+    __syncthreads();  // B2: w, r of all 32 rows visible
+
+    // ---- C: tile phase -----------------------------------------------------
+    if constexpr (DLSA_ABLATE != 1 && DLSA_ABLATE != 3)
+    static_for<W>([&](auto wI) {
+      constexpr int WID = decltype(wI)::value;
+      if (wid == WID) tile_phase<NT, W, PREC, STD, WID>(acc, xs, wr, p, ic, lane, stdv, obx);
+    });
+  }
+  wait_vmcnt<0>();  // drain the tail re-fetches
+  __syncthreads();
+
+  // ---- epilogue ------------------------------------------------------------
+  double* sH = a.slab_H + (int64_t)chunk * G::T * 256;
+  static_for<W>([&](auto wI) {
+    constexpr int WID = decltype(wI)::value;
+    if (wid == WID) store_tiles<NT, W, PREC, STD, WID>(acc, sH, lane);
+  });
+  // gradient: sum the row-lanes of each feature (xor LPR .. 32), then the waves
+  double* red = (double*)smem;  // ring is no longer needed: [W][PMAX] + [W]
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    double v = gacc[m];
+#pragma unroll
+    for (int o = LPR; o < 64; o <<= 1) v += __shfl_xor(v, o);
+    if (lane < LPR) red[wid * G::PMAX + sl + LPR * m] = v;
+  }
+#pragma unroll
+  for (int o = LPR; o < 64; o <<= 1) llacc += __shfl_xor(llacc, o);
+  if (lane == 0) red[W * G::PMAX + wid] = llacc;
+  __syncthreads();
+  for (int f = tid; f < G::PMAX; f += 64 * W) {
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) s += red[w * G::PMAX + f];
+    a.slab_g[(int64_t)chunk * G::PMAX + f] = s;
+  }
+  if (tid == 0) {
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) s += red[W * G::PMAX + w];
+    a.slab_ll[chunk] = s;
+  }
+}
+
+template <int NT, int W, int PREC, bool STD, int FAM>
+static hipError_t launch_c(const PassArgs& a, int n_chunks, hipStream_t s) {
+  auto kern = irls_coop_kernel<NT, W, PREC, STD, FAM>;
+  const size_t lds =
+      (size_t)a.nslot * a.slot_bytes + coop_extra_bytes_impl(NT);
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(n_chunks), dim3(64 * W), lds, s, a);
+  return hipGetLastError();
+}
+
+template <int NT, int W>
+static hipError_t launch_coop_ntw(const PassArgs& a, int prec, bool std_, int family,
+                                  int n_chunks, hipStream_t s) {
+  if (family == FAMILY_GAUSSIAN) {
+    if (prec != PREC_F64) return hipErrorInvalidValue;
+    return std_ ? launch_c<NT, W, PREC_F64, true, FAMILY_GAUSSIAN>(a, n_chunks, s)
+                : launch_c<NT, W, PREC_F64, false, FAMILY_GAUSSIAN>(a, n_chunks, s);
+  }
+  switch (prec) {
+    case PREC_BF16:
+      return std_ ? launch_c<NT, W, PREC_BF16, true, FAMILY_LOGISTIC>(a, n_chunks, s)
+                  : launch_c<NT, W, PREC_BF16, false, FAMILY_LOGISTIC>(a, n_chunks, s);
+    case PREC_F32:
+      return std_ ? launch_c<NT, W, PREC_F32, true, FAMILY_LOGISTIC>(a, n_chunks, s)
+                  : launch_c<NT, W, PREC_F32, false, FAMILY_LOGISTIC>(a, n_chunks, s);
+    default:
+      return std_ ? launch_c<NT, W, PREC_F64, true, FAMILY_LOGISTIC>(a, n_chunks, s)
+                  : launch_c<NT, W, PREC_F64, false, FAMILY_LOGISTIC>(a, n_chunks, s);
+  }
+}
+
+template <int NT>
+static hipError_t launch_coop_nt(const PassArgs& a, int prec, bool std_, int family,
+                                 int n_chunks, hipStream_t s) {
+  if constexpr (NT <= 8) {
+    if (coop_waves(NT) == 4) return launch_coop_ntw<NT, 4>(a, prec, std_, family, n_chunks, s);
+  }
+  return launch_coop_ntw<NT, 8>(a, prec, std_, family, n_chunks, s);
+}
+
+}  // namespace dlsa

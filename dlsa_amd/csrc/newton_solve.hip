@@ -5,7 +5,7 @@
 // 2 passes over X per CG step; here H is assembled once per pass and factored
 // in LDS):
 //   1. sum the chunk partials of the pass (fixed order -> deterministic),
-//      mirror the lower tiles into a full P x P matrix in LDS;
+//      keep the lower triangle packed in LDS (P <= 192: <= 152 KB);
 //   2. step control: if the log-likelihood fell, halve the previous step
 //      (the role of sklearn's line search);
 //   3. publish H as Sig_inv (models.py:130: the information at the point the
@@ -35,27 +35,32 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+// Packed lower triangle: element (i, j), i >= j, at i (i + 1) / 2 + j.
+__device__ __forceinline__ int tri(int i, int j) { return i * (i + 1) / 2 + j; }
+
 template <int NT>
 __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   constexpr int T = NT * (NT + 1) / 2;
   constexpr int PP = 16 * NT;
+  constexpr int R = (PP + 63) / 64;  // solve registers per lane (rows lane + 64 r)
   const int k = blockIdx.x;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
   if (a.status[k] != STATUS_RUNNING) return;  // block-uniform
   const int P = a.P;
-  const int LD = P + 1;
-  double* H = sm;            // P x LD
-  double* g = H + P * LD;    // PP
-  double* z = g + PP;        // PP
-  double* red = z + PP;      // 8: [0..3] block reductions, [6] flag, [7] ll
+  double* H = sm;                    // packed lower triangle, P (P + 1) / 2
+  double* g = H + P * (P + 1) / 2;   // PP
+  double* z = g + PP;                // PP
+  double* red = z + PP;              // 8: [0..3] block reductions, [6] flag, [7] ll
 
   const int cb = a.part_chunk_begin[k], ce = a.part_chunk_begin[k + 1];
   const int phase = a.phase[k];
 
   // 1. assemble: thread tid owns element (tile t, position tid) of every
-  //    tile; the chunk loop issues T independent loads per step
+  //    tile; the chunk loop issues T independent loads per step.  Only the
+  //    lower triangle is kept (diagonal tiles hold (w x_i) x_j and (w x_j) x_i,
+  //    equal up to the last bit): Sig_inv comes out exactly symmetric.
   {
     double acc[T];
 #pragma unroll
@@ -72,13 +77,7 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
       for (int J = 0; J <= I; ++J) {
         const int t = I * (I + 1) / 2 + J;
         const int gi = 16 * I + r, gj = 16 * J + q;
-        // lower triangle only (diagonal tiles hold (w x_i) x_j and
-        // (w x_j) x_i, equal up to the last bit): mirroring makes Sig_inv
-        // exactly symmetric
-        if (gi < P && gj < P && gi >= gj) {
-          H[gi * LD + gj] = acc[t];
-          H[gj * LD + gi] = acc[t];
-        }
+        if (gi < P && gi >= gj) H[tri(gi, gj)] = acc[t];
       }
   }
   if (tid < PP) {
@@ -137,44 +136,46 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
   if (!a.subsample) {
     double* S = a.sig_inv + (int64_t)k * P * P;
     for (int e = tid; e < P * P; e += 256) {
-      const int i = e / P;
-      S[e] = H[i * LD + (e - i * P)];
+      const int i = e / P, j = e - i * P;
+      S[e] = H[i >= j ? tri(i, j) : tri(j, i)];
     }
     if (tid == 0) a.loglik[k] = ll;
   }
   __syncthreads();
 
-  // 4. Cholesky, right-looking, lower, in place.  Thread (row = tid/2,
-  //    parity = tid%2) owns the even/odd columns of one row.  Column j is
-  //    only READ during step j (l_xj = H[x][j] / sqrt(H[j][j]) recomputed by
-  //    every reader); its scaled values are written back at step j+1, so one
+  // 4. Cholesky, right-looking, lower, in place.  Thread (tid/2, tid%2) owns
+  //    the even/odd columns of rows tid/2, tid/2 + 128.  Column j is only READ
+  //    during step j (l_xj = H[x][j] / sqrt(H[j][j]) recomputed by every
+  //    reader); its scaled values are written back at step j+1, so one
   //    barrier per column suffices.
-  const int row = tid >> 1, par = tid & 1;
+  const int row0 = tid >> 1, par = tid & 1;
   bool ok = true;
   double inv_prev = 0.0;
   for (int j = 0; j < P; ++j) {
-    const double d = H[j * LD + j];
+    const double d = H[tri(j, j)];
     if (!(d > 0.0) || !isfinite(d)) {
       ok = false;  // uniform: every thread read the same d
       break;
     }
-    const double ljj = sqrt(d);
-    const double inv = 1.0 / ljj;
-    if (row < P && par == 0 && j > 0 && row >= j - 1) {
-      // deferred write-back of column j-1 (scaled) for this row
-      H[row * LD + (j - 1)] = (row == j - 1) ? sqrt(H[row * LD + row]) : H[row * LD + (j - 1)] * inv_prev;
-    }
-    if (row < P && row > j) {
-      const double lij = H[row * LD + j] * inv;
-      for (int c = j + 1 + par; c <= row; c += 2)
-        H[row * LD + c] -= lij * (H[c * LD + j] * inv);
+    const double inv = 1.0 / sqrt(d);
+    const double* colj = H + j;  // H[tri(c, j)] = colj[c (c + 1) / 2]
+    for (int row = row0; row < P; row += 128) {
+      double* hr = H + tri(row, 0);
+      if (par == 0 && j > 0 && row >= j - 1) {
+        // deferred write-back of column j-1 (scaled) for this row
+        hr[j - 1] = (row == j - 1) ? sqrt(hr[row]) : hr[j - 1] * inv_prev;
+      }
+      if (row > j) {
+        const double lij = hr[j] * inv;
+        for (int c = j + 1 + par; c <= row; c += 2) hr[c] -= lij * (colj[tri(c, 0)] * inv);
+      }
     }
     inv_prev = inv;
     __syncthreads();
   }
-  if (ok && row < P && par == 0 && row >= P - 1) {
+  if (ok && par == 0 && row0 == (P - 1) % 128 && row0 < P) {
     // last column: only the diagonal element
-    H[row * LD + row] = sqrt(H[row * LD + row]);
+    H[tri(P - 1, P - 1)] = sqrt(H[tri(P - 1, P - 1)]);
   }
   __syncthreads();
   if (!ok) {
@@ -184,7 +185,7 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
     }
     if (tid == 0) {
       if (phase == PHASE_F32 && a.family == FAMILY_LOGISTIC) {
-        // fp32 Hessian lost definiteness: redo this point with fp64
+        // low-precision Hessian lost definiteness: redo this point with fp64
         a.phase[k] = PHASE_F64;
         a.iters[k] = it + 1;
         atomicAdd(&a.counters[PHASE_F64], 1);
@@ -196,28 +197,45 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
   }
 
   // 5. triangular solves L z = g, L^T d = z by wave 0 (no barriers: lane l
-  //    holds z[l] and z[l+64]; the pivot is broadcast by shuffle)
+  //    holds z[l + 64 r]; the pivot is broadcast by shuffle)
   if (wid == 0) {
-    double z0 = lane < P ? g[lane] : 0.0;
-    double z1 = lane + 64 < P ? g[lane + 64] : 0.0;
+    double zr[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) zr[r] = lane + 64 * r < P ? g[lane + 64 * r] : 0.0;
     for (int j = 0; j < P; ++j) {
-      const double zj = __shfl(j < 64 ? z0 : z1, j & 63) / H[j * LD + j];
-      if (lane == (j & 63)) {
-        if (j < 64) z0 = zj; else z1 = zj;
+      double piv = 0.0;
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if ((j >> 6) == r) piv = zr[r];
+      const double zj = __shfl(piv, j & 63) / H[tri(j, j)];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int i = lane + 64 * r;
+        if (i == j)
+          zr[r] = zj;
+        else if (i > j && i < P)
+          zr[r] -= H[tri(i, j)] * zj;
       }
-      if (lane > j && lane < P) z0 -= H[lane * LD + j] * zj;
-      if (lane + 64 > j && lane + 64 < P) z1 -= H[(lane + 64) * LD + j] * zj;
     }
     for (int j = P - 1; j >= 0; --j) {
-      const double zj = __shfl(j < 64 ? z0 : z1, j & 63) / H[j * LD + j];
-      if (lane == (j & 63)) {
-        if (j < 64) z0 = zj; else z1 = zj;
+      double piv = 0.0;
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if ((j >> 6) == r) piv = zr[r];
+      const double zj = __shfl(piv, j & 63) / H[tri(j, j)];
+      const double* lj = H + tri(j, 0);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int i = lane + 64 * r;
+        if (i == j)
+          zr[r] = zj;
+        else if (i < j)
+          zr[r] -= lj[i] * zj;
       }
-      if (lane < j) z0 -= H[j * LD + lane] * zj;
-      if (lane + 64 < j) z1 -= H[j * LD + lane + 64] * zj;
     }
-    if (lane < P) z[lane] = z0;
-    if (lane + 64 < P) z[lane + 64] = z1;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (lane + 64 * r < P) z[lane + 64 * r] = zr[r];
   }
   __syncthreads();
 
@@ -306,7 +324,7 @@ static hipError_t launch_solve_t(const SolveArgs& a, int K, size_t lds, hipStrea
 
 hipError_t launch_newton_solve(const SolveArgs& a, int K, hipStream_t s) {
   const int PP = 16 * a.NT;
-  const size_t lds = ((size_t)a.P * (a.P + 1) + 2 * PP + 8) * sizeof(double);
+  const size_t lds = ((size_t)a.P * (a.P + 1) / 2 + 2 * PP + 8) * sizeof(double);
   switch (a.NT) {
     case 1: return launch_solve_t<1>(a, K, lds, s);
     case 2: return launch_solve_t<2>(a, K, lds, s);
@@ -316,6 +334,10 @@ hipError_t launch_newton_solve(const SolveArgs& a, int K, hipStream_t s) {
     case 6: return launch_solve_t<6>(a, K, lds, s);
     case 7: return launch_solve_t<7>(a, K, lds, s);
     case 8: return launch_solve_t<8>(a, K, lds, s);
+    case 9: return launch_solve_t<9>(a, K, lds, s);
+    case 10: return launch_solve_t<10>(a, K, lds, s);
+    case 11: return launch_solve_t<11>(a, K, lds, s);
+    case 12: return launch_solve_t<12>(a, K, lds, s);
     default: return hipErrorInvalidValue;
   }
 }

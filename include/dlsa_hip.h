@@ -66,7 +66,7 @@ extern "C" {
 #define DLSA_HESSIAN_MIXED_F32 2  /* as MIXED with fp32 MFMA approximate passes
                                      (for ill-conditioned designs) */
 
-#define DLSA_MAX_P_FUSED 128  /* largest P handled by the per-wave fused pass */
+#define DLSA_MAX_P_FUSED 192  /* largest P handled by the fused pass + LDS Newton solve */
 
 typedef struct dlsa_fit_options {
   int32_t hessian_mode;     /* DLSA_HESSIAN_MIXED (default) or _FP64 */

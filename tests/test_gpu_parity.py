@@ -129,11 +129,15 @@ def test_device_generator_matches_host(torch_cuda, M):
 
 
 @pytest.mark.parametrize("p,fi", [(1, False), (1, True), (15, True), (16, False), (16, True),
-                                  (33, False), (64, True), (100, False), (127, True), (128, False)])
+                                  (33, False), (64, True), (100, False), (127, True), (128, False),
+                                  (129, False), (150, True), (181, True), (192, False)])
 def test_shapes_vs_oracle(torch_cuda, M, p, fi):
-    """Every column-tile count NT = 1..8 and the partial-tile / intercept
-    edges, ragged partition sizes (incl. one < 8 rows block tail)."""
+    """Column-tile counts NT = 1..12 (4-wave and 8-wave pass geometries) and
+    the partial-tile / intercept edges, ragged partition sizes (incl. a block
+    tail of < 8 rows)."""
     sizes = [3001, 1500, 4096, 2003]
+    if p > 128:  # keep n_k / P well above the MLE-existence threshold
+        sizes = [4 * s + 1 for s in sizes]
     n = sum(sizes)
     X, y = O.simulate_counter(n, p, seed=p * 7 + fi)
     off = np.concatenate([[0], np.cumsum(sizes)])

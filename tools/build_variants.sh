@@ -1,6 +1,6 @@
 #!/bin/bash
 # Profiling-only builds of libdlsa_hip.so with DLSA_ABLATE=1/2/3 (see
-# dlsa_amd/csrc/irls_pass.hip).  Output: tools/_variants/*.so (git-ignored).
+# dlsa_amd/csrc/irls_pass.hip and irls_coop.hip).  Output: tools/_variants/*.so (git-ignored).
 set -e
 cd "$(dirname "$0")/.."
 for v in "$@"; do
@@ -8,8 +8,8 @@ for v in "$@"; do
     ablate1) D=DLSA_ABLATE=1 ;;
     ablate2) D=DLSA_ABLATE=2 ;;
     ablate3) D=DLSA_ABLATE=3 ;;
+    ablate4) D=DLSA_ABLATE=4 ;;
     *) echo "unknown variant $v"; exit 1 ;;
   esac
-  python -c "from dlsa_amd.build import build; print(build(force=True, out='tools/_variants/libdlsa_hip_$v.so', defines=['$D']))" &
+  python -c "from dlsa_amd.build import build; print(build(force=True, out='tools/_variants/libdlsa_hip_$v.so', defines=['$D']))"
 done
-wait

@@ -44,6 +44,7 @@ def main():
                     help='";"-separated configs of ","-separated ENV=VAL; "default" = none')
     ap.add_argument("--hessian", default="mixed")
     ap.add_argument("--rows-per-chunk", type=int, default=0)
+    ap.add_argument("--warm", type=int, default=0, help="warm-start levels (0: full-row passes only)")
     args = ap.parse_args()
 
     import numpy as np
@@ -86,6 +87,7 @@ def main():
                 opt.hessian_mode = 1 if args.hessian == "fp64" else 0
                 opt.record_timing = 1
                 opt.rows_per_chunk = args.rows_per_chunk
+                opt.warm_start = args.warm
                 opt.workspace = ws.data_ptr()
                 opt.workspace_bytes = ws.numel()
                 rc = lib.dlsa_logistic_fit_batched_ex(
@@ -102,6 +104,7 @@ def main():
                 if s.passes_fp64:
                     d["f64"].append(s.ms_pass_fp64 / s.passes_fp64)
                 d["solve"].append(s.ms_solve / max(1, s.iterations))
+                d.setdefault("total", []).append(s.ms_total)
                 d["it"].append((s.passes_fp32, s.passes_fp64))
                 for kv in [x for x in kn.split(",") if x]:
                     os.environ.pop(kv.split("=")[0], None)
@@ -113,6 +116,7 @@ def main():
                 out[f"{key}_ms"] = round(m, 3)
                 out[f"{key}_GBps"] = round(bytes_per_pass / (m * 1e-3) / 1e9, 1)
         out["solve_ms_per_iter"] = round(statistics.median(d["solve"]), 3)
+        out["fit_ms"] = round(statistics.median(d["total"]), 2)
         print(json.dumps(out), flush=True)
 
 
