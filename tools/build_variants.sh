@@ -2,6 +2,7 @@
 # Profiling-only builds of libdlsa_hip.so with DLSA_ABLATE=1/2/3 (see
 # dlsa_amd/csrc/irls_pass.hip and irls_coop.hip).  Output: tools/_variants/*.so (git-ignored).
 set -e
+mkdir -p tools/_variants
 cd "$(dirname "$0")/.."
 for v in "$@"; do
   case $v in
