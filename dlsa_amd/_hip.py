@@ -22,6 +22,7 @@ HESSIAN_MIXED = 0
 HESSIAN_FP64 = 1
 HESSIAN_MIXED_F32 = 2
 MAX_P_FUSED = 192
+MAX_P = 512
 
 
 class DlsaHipError(RuntimeError):
@@ -53,6 +54,9 @@ class FitStats(ctypes.Structure):
         ("ms_total", ctypes.c_double),
         ("rows_fp32", ctypes.c_int64),
         ("rows_fp64", ctypes.c_int64),
+        ("ms_wide_row", ctypes.c_double),
+        ("ms_wide_gram", ctypes.c_double),
+        ("ms_wide_assemble", ctypes.c_double),
     ]
 
     def as_dict(self):

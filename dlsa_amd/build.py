@@ -19,7 +19,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libdlsa_hip.so")
 SOURCES = (["irls_pass.hip", "irls_coop.hip"] + [f"irls_coop_g{i}.hip" for i in range(1, 7)] +
-           ["eval_pass.hip", "newton_solve.hip", "aux_kernels.hip", "capi.hip", "lars_host.cpp"])
+           ["wide_pass.hip", "eval_pass.hip", "newton_solve.hip", "aux_kernels.hip", "capi.hip", "lars_host.cpp"])
 HEADERS = ["dlsa_internal.hpp", "irls_coop_impl.hpp", os.path.join("..", "..", "include", "dlsa_hip.h")]
 ARCH = os.environ.get("DLSA_OFFLOAD_ARCH", "gfx950")
 

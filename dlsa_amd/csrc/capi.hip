@@ -128,6 +128,75 @@ static Layout make_layout(const Plan& pl, int K) {
   return L;
 }
 
+// ---- wide-P path (P > DLSA_MAX_P_FUSED): row chunks + Gram row groups ------
+struct WidePlans {
+  Plan rows, gram;
+};
+
+// Row pass: ~2048 chunks (one 256-thread workgroup each, HBM-bound).  Gram
+// pass: ~1024 (row group, tile) workgroups, a multiple of 8 row groups so the
+// XCD-aware mapping fills every XCD.
+static void make_wide_plans(const int64_t* offsets, int K, int p, int intercept,
+                            int rows_per_chunk, WidePlans& wp, double frac = 1.0,
+                            int64_t min_rows = 0) {
+  const int64_t n_total = offsets[K];
+  const int P = p + (intercept ? 1 : 0);
+  const int NB = (P + kWideTile - 1) / kWideTile;
+  const int TB = NB * (NB + 1) / 2;
+  int rpc_row = (int)std::max<int64_t>(256, std::min<int64_t>(n_total / 2048, 16384));
+  int64_t groups = ((1024 + TB - 1) / TB + 7) / 8 * 8;
+  int rpc_gram = (int)std::max<int64_t>(1024, std::min<int64_t>((n_total + groups - 1) / groups,
+                                                                int64_t(1) << 24));
+  if (rows_per_chunk > 0) rpc_row = rpc_gram = rows_per_chunk;
+  if (const char* e = getenv("DLSA_WIDE_GRAM_ROWS")) rpc_gram = std::max(64, atoi(e));
+  make_plan(offsets, K, p, intercept, rpc_row, wp.rows, frac, min_rows);
+  make_plan(offsets, K, p, intercept, rpc_gram, wp.gram, frac, min_rows);
+}
+
+struct WideLayout {
+  int64_t off_r_row0, off_r_rows, off_r_part, off_rcb;
+  int64_t off_g_row0, off_g_rows, off_g_part, off_gcb;
+  int64_t off_offsets, off_w, off_slabg, off_slabll, off_slabG, off_H;
+  int64_t off_phase, off_bt, off_llprev, off_thprev, off_dprev, off_counters;
+  int64_t total;
+};
+
+static WideLayout make_wide_layout(const WidePlans& wp, int K, int64_t n_total, int P) {
+  const int NB = (P + kWideTile - 1) / kWideTile;
+  const int64_t PP = (int64_t)kWideTile * NB;
+  const int64_t TB = NB * (NB + 1) / 2;
+  const int64_t nr = std::max(wp.rows.n_chunks, 1), ng = std::max(wp.gram.n_chunks, 1);
+  WideLayout L;
+  int64_t o = 0;
+  auto take = [&](int64_t bytes) {
+    int64_t r = o;
+    o = align_up(o + bytes, 256);
+    return r;
+  };
+  L.off_r_row0 = take(8 * nr);
+  L.off_r_rows = take(4 * nr);
+  L.off_r_part = take(4 * nr);
+  L.off_rcb = take(4LL * (K + 1));
+  L.off_g_row0 = take(8 * ng);
+  L.off_g_rows = take(4 * ng);
+  L.off_g_part = take(4 * ng);
+  L.off_gcb = take(4LL * (K + 1));
+  L.off_offsets = take(8LL * (K + 1));
+  L.off_w = take(8 * std::max<int64_t>(n_total, 1));
+  L.off_slabg = take(8 * nr * PP);
+  L.off_slabll = take(8 * nr);
+  L.off_slabG = take(8 * ng * TB * kWideTile * kWideTile);
+  L.off_H = take(8LL * K * PP * PP);
+  L.off_phase = take(4LL * K);
+  L.off_bt = take(4LL * K);
+  L.off_llprev = take(8LL * K);
+  L.off_thprev = take(8LL * K * P);
+  L.off_dprev = take(8LL * K * P);
+  L.off_counters = take(16);
+  L.total = o;
+  return L;
+}
+
 static int check_offsets(const int64_t* offsets, int K) {
   if (!offsets || K < 1) {
     set_error("offsets must be a host array of K+1 >= 2 entries");
@@ -174,6 +243,12 @@ const char* dlsa_build_info(void) {
 int64_t dlsa_logistic_workspace_bytes(const int64_t* offsets, int32_t K, int32_t p,
                                       int32_t fit_intercept, int32_t rows_per_chunk) {
   if (check_offsets(offsets, K) != DLSA_OK) return -1;
+  const int P = p + (fit_intercept ? 1 : 0);
+  if (P > DLSA_MAX_P_FUSED) {
+    WidePlans wp;
+    make_wide_plans(offsets, K, p, fit_intercept, rows_per_chunk, wp);
+    return make_wide_layout(wp, K, offsets[K], P).total;
+  }
   Plan pl;
   make_plan(offsets, K, p, fit_intercept, rows_per_chunk, pl);
   return make_layout(pl, K).total;
@@ -188,6 +263,237 @@ int dlsa_last_fit_stats(dlsa_fit_stats* out) {
 }  // extern "C"
 
 namespace dlsa {
+
+// Event timer of the fit's stream (record_timing only).
+struct StreamTimer {
+  hipStream_t stream;
+  bool on;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  hipError_t init() {
+    if (!on) return hipSuccess;
+    hipError_t e = hipEventCreate(&ev[0]);
+    if (e == hipSuccess) e = hipEventCreate(&ev[1]);
+    return e;
+  }
+  ~StreamTimer() {
+    if (ev[0]) (void)hipEventDestroy(ev[0]);
+    if (ev[1]) (void)hipEventDestroy(ev[1]);
+  }
+  template <typename F>
+  hipError_t operator()(double* acc, F&& launch) {
+    if (!on) return launch();
+    hipError_t e = hipEventRecord(ev[0], stream);
+    if (e == hipSuccess) e = launch();
+    if (e == hipSuccess) e = hipEventRecord(ev[1], stream);
+    if (e == hipSuccess) e = hipEventSynchronize(ev[1]);
+    float ms = 0.f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, ev[0], ev[1]);
+    *acc += ms;
+    return e;
+  }
+};
+
+// P > DLSA_MAX_P_FUSED (wide_pass.hip): per Newton iteration a row pass, a
+// Gram pass per running precision phase, the deterministic partial-tile
+// assembly and the per-partition blocked-Cholesky update.  Same warm-start
+// levels, phases, state machine and outputs as the fused path.
+static int fit_wide(int family, const double* X, const double* y, const int64_t* offsets,
+                    int32_t K, int32_t p, int32_t fit_intercept, const double* center,
+                    const double* scale, int32_t max_iter, double tol, double* theta,
+                    double* sig_inv, double* sig_inv_theta, double* loglik, int32_t* iters,
+                    int32_t* status, const dlsa_fit_options& opt, hipStream_t stream,
+                    std::chrono::steady_clock::time_point t_start) {
+  const int P = p + (fit_intercept ? 1 : 0);
+  const int NB = (P + kWideTile - 1) / kWideTile;
+  const int64_t n_total = offsets[K];
+  WidePlans fin;
+  make_wide_plans(offsets, K, p, fit_intercept, opt.rows_per_chunk, fin);
+  const WideLayout L = make_wide_layout(fin, K, n_total, P);
+  g_stats.n_chunks = fin.gram.n_chunks;
+
+  char* ws = (char*)opt.workspace;
+  bool owned = false;
+  if (!ws) {
+    DLSA_HIP_TRY(hipMallocAsync((void**)&ws, L.total, stream));
+    owned = true;
+  } else if (opt.workspace_bytes < L.total) {
+    set_error("workspace too small: need " + std::to_string(L.total) + " bytes");
+    return DLSA_E_WORKSPACE;
+  }
+  struct Free {
+    char* p;
+    bool own;
+    hipStream_t s;
+    ~Free() {
+      if (own && p) (void)hipFreeAsync(p, s);
+    }
+  } freer{ws, owned, stream};
+  auto at = [&](int64_t off) { return (void*)(ws + off); };
+  int64_t* d_offsets = (int64_t*)at(L.off_offsets);
+  int32_t* d_rcb = (int32_t*)at(L.off_rcb);
+  int32_t* d_gcb = (int32_t*)at(L.off_gcb);
+  double* d_H = (double*)at(L.off_H);
+  int32_t* d_phase = (int32_t*)at(L.off_phase);
+  int32_t* d_bt = (int32_t*)at(L.off_bt);
+  double* d_llprev = (double*)at(L.off_llprev);
+  int32_t* d_cnt = (int32_t*)at(L.off_counters);
+
+  WideArgs wa;
+  memset(&wa, 0, sizeof(wa));
+  wa.X = X;
+  wa.y = y;
+  wa.rc_row0 = (const int64_t*)at(L.off_r_row0);
+  wa.rc_rows = (const int32_t*)at(L.off_r_rows);
+  wa.rc_part = (const int32_t*)at(L.off_r_part);
+  wa.gc_row0 = (const int64_t*)at(L.off_g_row0);
+  wa.gc_rows = (const int32_t*)at(L.off_g_rows);
+  wa.gc_part = (const int32_t*)at(L.off_g_part);
+  wa.phase = d_phase;
+  wa.theta = theta;
+  wa.center = center;
+  wa.scale = scale;
+  wa.w = (double*)at(L.off_w);
+  wa.slab_g = (double*)at(L.off_slabg);
+  wa.slab_ll = (double*)at(L.off_slabll);
+  wa.slab_G = (double*)at(L.off_slabG);
+  wa.p = p;
+  wa.P = P;
+  wa.intercept = fit_intercept ? 1 : 0;
+  wa.NB = NB;
+
+  auto upload_plan = [&](const Plan& q, int64_t o_row0, int64_t o_rows, int64_t o_part,
+                         int32_t* d_cb) -> hipError_t {
+    hipError_t e = hipSuccess;
+    if (q.n_chunks > 0) {
+      e = hipMemcpyAsync(at(o_row0), q.chunk_row0.data(), 8LL * q.n_chunks,
+                         hipMemcpyHostToDevice, stream);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(at(o_rows), q.chunk_rows.data(), 4LL * q.n_chunks,
+                           hipMemcpyHostToDevice, stream);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(at(o_part), q.chunk_part.data(), 4LL * q.n_chunks,
+                           hipMemcpyHostToDevice, stream);
+    }
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(d_cb, q.part_chunk_begin.data(), 4LL * (K + 1), hipMemcpyHostToDevice,
+                         stream);
+    return e;
+  };
+  DLSA_HIP_TRY(hipMemcpyAsync(d_offsets, offsets, 8LL * (K + 1), hipMemcpyHostToDevice, stream));
+
+  std::vector<WidePlans> plans;
+  if (family == FAMILY_LOGISTIC && opt.warm_start) {
+    const int64_t min_rows = std::max<int64_t>(2048, 64LL * P);
+    for (double frac : {1.0 / 16.0, 1.0 / 4.0}) {
+      WidePlans q;
+      make_wide_plans(offsets, K, p, fit_intercept, opt.rows_per_chunk, q, frac, min_rows);
+      int64_t rows = 0;
+      for (int c = 0; c < q.rows.n_chunks; ++c) rows += q.rows.chunk_rows[c];
+      if (rows <= n_total / 2 && q.rows.n_chunks > 0) plans.push_back(std::move(q));
+    }
+  }
+  plans.push_back(fin);
+
+  // the Gram pass has an fp64 MFMA variant only: every wide fit runs its
+  // Newton passes with the fp64 Hessian
+  const int start_phase = PHASE_F64;
+  DLSA_HIP_TRY(launch_fit_init(d_offsets, K, P, start_phase, theta, d_phase, d_bt, iters, status,
+                               d_llprev, sig_inv, loglik, stream));
+  int n_running[2] = {0, 0};
+  for (int k = 0; k < K; ++k)
+    if (offsets[k + 1] > offsets[k]) n_running[start_phase]++;
+
+  SolveArgs sa;
+  memset(&sa, 0, sizeof(sa));
+  sa.theta = theta;
+  sa.theta_prev = (double*)at(L.off_thprev);
+  sa.delta_prev = (double*)at(L.off_dprev);
+  sa.ll_prev = d_llprev;
+  sa.phase = d_phase;
+  sa.backtracks = d_bt;
+  sa.iters = iters;
+  sa.status = status;
+  sa.counters = d_cnt;
+  sa.sig_inv = sig_inv;
+  sa.loglik = loglik;
+  sa.P = P;
+  sa.family = family;
+  sa.tol = tol;
+  sa.switch_tol = opt.switch_tol;
+
+  const bool standardize = center != nullptr;
+  StreamTimer timed{stream, opt.record_timing != 0};
+  DLSA_HIP_TRY(timed.init());
+  int32_t* h_cnt = nullptr;
+  DLSA_HIP_TRY(hipHostMalloc((void**)&h_cnt, 16, hipHostMallocDefault));
+  struct HFree {
+    int32_t* p;
+    ~HFree() {
+      if (p) (void)hipHostFree(p);
+    }
+  } hfree{h_cnt};
+
+  int it = 0;
+  for (size_t lvl = 0; lvl < plans.size(); ++lvl) {
+    const WidePlans& q = plans[lvl];
+    const bool final_level = lvl + 1 == plans.size();
+    DLSA_HIP_TRY(upload_plan(q.rows, L.off_r_row0, L.off_r_rows, L.off_r_part, d_rcb));
+    DLSA_HIP_TRY(upload_plan(q.gram, L.off_g_row0, L.off_g_rows, L.off_g_part, d_gcb));
+    wa.n_gchunks = q.gram.n_chunks;
+    int64_t rows = 0;
+    for (int c = 0; c < q.rows.n_chunks; ++c) rows += q.rows.chunk_rows[c];
+    if (lvl > 0) {
+      DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
+      DLSA_HIP_TRY(launch_level_reset(K, P, start_phase, d_phase, status, d_llprev, d_bt, theta,
+                                      d_cnt, stream));
+      DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, stream));
+      DLSA_HIP_TRY(hipStreamSynchronize(stream));
+      n_running[0] = h_cnt[0];
+      n_running[1] = h_cnt[1];
+    }
+    sa.subsample = final_level ? 0 : 1;
+    sa.level_tol = 1e-2;
+    sa.switch_tol = final_level ? opt.switch_tol : 0.0;
+    const int it_end = final_level ? max_iter : std::min(max_iter, it + 10);
+    for (; it < it_end && (n_running[0] + n_running[1]) > 0 && q.rows.n_chunks > 0; ++it) {
+      double ms_row = 0.0, ms_gram = 0.0;
+      DLSA_HIP_TRY(timed(&ms_row, [&] {
+        return launch_wide_row(wa, standardize, family, q.rows.n_chunks, stream);
+      }));
+      for (int ph = 0; ph < 2; ++ph) {
+        if (n_running[ph] == 0) continue;
+        wa.want_phase = ph;
+        DLSA_HIP_TRY(timed(&ms_gram, [&] { return launch_wide_gram(wa, standardize, stream); }));
+        if (ph == PHASE_F64) {
+          g_stats.passes_fp64++;
+          g_stats.rows_fp64 += rows;
+        } else {
+          g_stats.passes_fp32++;
+          g_stats.rows_fp32 += rows;
+        }
+      }
+      g_stats.ms_wide_row += ms_row;
+      g_stats.ms_wide_gram += ms_gram;
+      g_stats.ms_pass_fp64 += ms_row + ms_gram;
+      DLSA_HIP_TRY(timed(&g_stats.ms_wide_assemble,
+                         [&] { return launch_wide_assemble(wa, d_gcb, d_H, K, stream); }));
+      DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
+      DLSA_HIP_TRY(timed(&g_stats.ms_solve,
+                         [&] { return launch_wide_newton(sa, wa, d_rcb, d_H, K, stream); }));
+      DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, stream));
+      DLSA_HIP_TRY(hipStreamSynchronize(stream));
+      n_running[0] = h_cnt[0];
+      n_running[1] = h_cnt[1];
+    }
+  }
+  g_stats.iterations = it;
+  DLSA_HIP_TRY(launch_fit_finalize(K, P, theta, sig_inv, sig_inv_theta, status, stream));
+  DLSA_HIP_TRY(hipStreamSynchronize(stream));
+  g_stats.ms_total =
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start)
+          .count();
+  return DLSA_OK;
+}
 
 static int fit_impl(int family, const double* X, const double* y, const int64_t* offsets,
                     int32_t K, int32_t p, int32_t fit_intercept, const double* center,
@@ -212,9 +518,8 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
     return DLSA_E_INVALID;
   }
   const int P = p + (fit_intercept ? 1 : 0);
-  if (P > DLSA_MAX_P_FUSED) {
-    set_error("P = p + intercept > " + std::to_string(DLSA_MAX_P_FUSED) +
-              " is not supported by the fused pass yet");
+  if (P > DLSA_MAX_P) {
+    set_error("P = p + intercept > " + std::to_string(DLSA_MAX_P) + " is not supported");
     return DLSA_E_UNSUPPORTED;
   }
   if ((center == nullptr) != (scale == nullptr)) {
@@ -232,6 +537,10 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
   }
   if (max_iter < 1) max_iter = 1;
   if (!(tol > 0)) tol = 1e-10;
+  if (family == FAMILY_GAUSSIAN) max_iter = 1;  // closed form: one exact fp64 pass
+  if (P > DLSA_MAX_P_FUSED)
+    return fit_wide(family, X, y, offsets, K, p, fit_intercept, center, scale, max_iter, tol,
+                    theta, sig_inv, sig_inv_theta, loglik, iters, status, opt, stream, t_start);
 
   Plan pl;
   make_plan(offsets, K, p, fit_intercept, opt.rows_per_chunk, pl);

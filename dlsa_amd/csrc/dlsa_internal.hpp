@@ -93,7 +93,42 @@ struct EvalArgs {
   int32_t nslot, slot_bytes;
 };
 
+// Wide-P path (DLSA_MAX_P_FUSED < P <= DLSA_MAX_P, wide_pass.hip): a row
+// pass (eta, weights, gradient, log-lik) and a separate Gram pass over
+// 128x128 output tiles of the padded PP = 128 * NB Hessian.
+constexpr int kWideTile = 128;
+struct WideArgs {
+  const double* X;
+  const double* y;
+  const int64_t* rc_row0;  // row-pass chunks
+  const int32_t* rc_rows;
+  const int32_t* rc_part;
+  const int64_t* gc_row0;  // Gram-pass row groups
+  const int32_t* gc_rows;
+  const int32_t* gc_part;
+  const int32_t* phase;    // [K]
+  const double* theta;     // [K, P]
+  const double* center;    // [p] or null
+  const double* scale;
+  double* w;               // [n_total] IRLS weight of each row (row pass -> Gram pass)
+  double* slab_g;          // [n_rchunks, PP] partial gradients
+  double* slab_ll;         // [n_rchunks] partial log-likelihoods
+  double* slab_G;          // [n_gchunks, TB, 128 * 128] partial Gram tiles
+  int32_t p, P, intercept;
+  int32_t NB;              // 128-wide column blocks, PP = 128 NB
+  int32_t want_phase;      // Gram pass: partitions in this phase
+  int32_t n_gchunks;
+};
+
 // Launchers (defined in the .hip files).
+hipError_t launch_wide_row(const WideArgs& a, bool standardize, int family, int n_chunks,
+                           hipStream_t s);
+hipError_t launch_wide_gram(const WideArgs& a, bool standardize, hipStream_t s);
+hipError_t launch_wide_assemble(const WideArgs& a, const int32_t* gcb, double* Hfull, int K,
+                                hipStream_t s);
+hipError_t launch_wide_newton(const SolveArgs& sa, const WideArgs& wa, const int32_t* rcb,
+                              double* Hfull, int K, hipStream_t s);
+int wide_newton_lds_bytes(int NB);
 hipError_t launch_loglik_eval(const EvalArgs& a, int n_chunks, hipStream_t s);
 hipError_t launch_loglik_reduce(const double* partial, const int32_t* pcb, int K, int B,
                                 double* out, hipStream_t s);

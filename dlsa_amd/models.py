@@ -186,8 +186,8 @@ def logistic_model_batched(X, y, offsets, fit_intercept=False, center=None, scal
     if yd.numel() != n:
         raise ValueError("y must have n entries")
     P = p + (1 if fit_intercept else 0)
-    if P > _hip.MAX_P_FUSED:
-        raise DlsaHipError(f"P = {P} > {_hip.MAX_P_FUSED} not supported by the fused pass yet")
+    if P > _hip.MAX_P:
+        raise DlsaHipError(f"P = {P} > {_hip.MAX_P} is not supported")
     cd = sd = None
     if center is not None or scale is not None:
         cd = _dev_f64(center, dev).reshape(-1)
@@ -242,8 +242,8 @@ def ols_model_batched(X, y, offsets, fit_intercept=False, center=None, scale=Non
     if K < 1 or offs[0] != 0 or offs[-1] != n or np.any(np.diff(offs) < 0) or yd.numel() != n:
         raise ValueError("offsets must be non-decreasing, start at 0 and end at n; y has n rows")
     P = p + (1 if fit_intercept else 0)
-    if P > _hip.MAX_P_FUSED:
-        raise DlsaHipError(f"P = {P} > {_hip.MAX_P_FUSED} not supported by the fused pass yet")
+    if P > _hip.MAX_P:
+        raise DlsaHipError(f"P = {P} > {_hip.MAX_P} is not supported")
     cd = sd = None
     if center is not None or scale is not None:
         cd = _dev_f64(center, dev).reshape(-1)

@@ -67,6 +67,9 @@ extern "C" {
                                      (for ill-conditioned designs) */
 
 #define DLSA_MAX_P_FUSED 192  /* largest P handled by the fused pass + LDS Newton solve */
+#define DLSA_MAX_P 512        /* largest P overall: above DLSA_MAX_P_FUSED a row pass, a
+                                 128x128-tiled Gram pass and a blocked Cholesky in HBM
+                                 take over (BASELINE config 5, p = 500) */
 
 typedef struct dlsa_fit_options {
   int32_t hessian_mode;     /* DLSA_HESSIAN_MIXED (default) or _FP64 */
@@ -98,6 +101,10 @@ typedef struct dlsa_fit_stats {
   int64_t rows_fp32;        /* rows streamed by approximate-Hessian passes (sum
                                over launches, warm-start levels included) */
   int64_t rows_fp64;        /* rows streamed by fp64 passes (sum) */
+  double ms_wide_row;       /* P > DLSA_MAX_P_FUSED: row-pass kernel time (included
+                               in ms_pass_fp32/fp64 with the Gram pass) */
+  double ms_wide_gram;      /* P > DLSA_MAX_P_FUSED: Gram-pass kernel time */
+  double ms_wide_assemble;  /* P > DLSA_MAX_P_FUSED: partial-tile assembly time */
 } dlsa_fit_stats;
 
 /* Default options (mixed Hessian, automatic chunking, no timing). */
@@ -126,7 +133,7 @@ int64_t dlsa_logistic_workspace_bytes(const int64_t* offsets, int32_t K,
  *  theta          [K, P] out     sig_inv       [K, P, P] out
  *  sig_inv_theta  [K, P] out     loglik        [K] out (at theta)
  *  iters          [K] int32 out  status        [K] int32 out (DLSA_STATUS_*)
- * 1 <= P <= DLSA_MAX_P_FUSED.
+ * 1 <= P <= DLSA_MAX_P.
  */
 int dlsa_logistic_fit_batched(const double* X, const double* y,
                               const int64_t* offsets, int32_t K, int32_t p,

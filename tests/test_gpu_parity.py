@@ -295,3 +295,117 @@ def test_logistic_model_eval_reference_signature(torch_cuda, M):
     ref = O.logistic_loglik(X, y, par.to_numpy().T, fit_intercept=True)
     assert list(out.columns) == list(par.columns)
     assert np.abs(out.to_numpy()[0] - ref).max() <= 1e-10 * np.abs(ref).max()
+
+
+# ---- wide P (DLSA_MAX_P_FUSED < P <= DLSA_MAX_P): row pass + tiled Gram pass
+# + blocked Cholesky in HBM (BASELINE config 5 path) ---------------------------
+
+@pytest.mark.parametrize("p,fi,std", [(193, False, False), (200, True, False), (256, False, False),
+                                      (300, True, True), (383, True, False), (450, False, False),
+                                      (499, True, False), (512, False, False)])
+def test_wide_shapes_vs_oracle(torch_cuda, M, p, fi, std):
+    """NB = 2..4 column blocks of 128, partial last block / intercept edges,
+    several row chunks and Gram row groups per partition (row-group count not
+    a multiple of 8), ragged partitions."""
+    sizes = [10 * p + 7, 12 * p + 1001, 11 * p]
+    n = sum(sizes)
+    X, y = O.simulate_counter(n, p, seed=p * 3 + fi)
+    center = scale = None
+    if std:
+        X = X * 2.0 + 0.25
+        center, scale = X.mean(0), X.std(0)
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    fit = M.logistic_model_batched(X, y, off, fit_intercept=fi, center=center, scale=scale,
+                                   rows_per_chunk=1000)
+    th, S, St, ll, it = O.logistic_fit_partitions(X, y, off, fit_intercept=fi, center=center,
+                                                  scale=scale)
+    assert (fit.status.cpu().numpy() == 0).all()
+    assert _rel(fit.theta.cpu(), th) < REL
+    assert _rel(fit.sig_inv.cpu(), S) < REL
+    assert _rel(fit.sig_inv_theta.cpu(), St) < REL
+    assert _rel(fit.loglik.cpu(), ll) < 1e-10
+    S_ = fit.sig_inv.cpu().numpy()
+    assert np.array_equal(S_, np.transpose(S_, (0, 2, 1)))
+
+
+def test_wide_auto_chunking_and_determinism(torch_cuda, M):
+    """Default (automatic) row-chunk / row-group plan, and bit-identical
+    results across two runs (fixed-order reductions everywhere)."""
+    torch = torch_cuda
+    p, K, nk = 260, 5, 6000
+    X, y = M.simulate_logistic_device(K * nk, p, seed=77)
+    off = np.arange(K + 1, dtype=np.int64) * nk
+    f1 = M.logistic_model_batched(X, y, off, fit_intercept=True)
+    f2 = M.logistic_model_batched(X, y, off, fit_intercept=True)
+    assert torch.equal(f1.theta, f2.theta) and torch.equal(f1.sig_inv, f2.sig_inv)
+    Xh, yh = X.cpu().numpy(), y.cpu().numpy()
+    for k in (0, 4):
+        o = O.logistic_fit(Xh[off[k]:off[k + 1]], yh[off[k]:off[k + 1]], fit_intercept=True)
+        assert _rel(f1.theta[k].cpu(), o["coef"]) < REL
+        assert _rel(f1.sig_inv[k].cpu(), o["Sig_inv"]) < REL
+
+
+def test_wide_edge_partitions(torch_cuda, M):
+    """Empty partition -> zero block; a partition with fewer rows than
+    parameters -> singular, the others unaffected."""
+    p = 220
+    sizes = [4000, 0, 150, 3500]
+    n = sum(sizes)
+    X, y = O.simulate_counter(n, p, seed=19)
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    fit = M.logistic_model_batched(X, y, off, max_iter=30, rows_per_chunk=700)
+    st = fit.status.cpu().numpy()
+    assert st[1] == 3
+    assert np.all(fit.sig_inv[1].cpu().numpy() == 0)
+    assert st[2] != 0
+    for k in (0, 3):
+        o = O.logistic_fit(X[off[k]:off[k + 1]], y[off[k]:off[k + 1]])
+        assert st[k] == 0
+        assert _rel(fit.theta[k].cpu(), o["coef"]) < REL
+        assert _rel(fit.sig_inv[k].cpu(), o["Sig_inv"]) < REL
+
+
+@pytest.mark.parametrize("p,fi", [(300, True), (500, False)])
+def test_wide_ols_vs_oracle(torch_cuda, M, p, fi):
+    rs = np.random.RandomState(p)
+    sizes = [4 * p, 3 * p + 11]
+    n = sum(sizes)
+    X = rs.rand(n, p) - 0.5
+    y = X @ rs.randn(p) + 0.3 + 0.1 * rs.randn(n)
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    fit = M.ols_model_batched(X, y, off, fit_intercept=fi, rows_per_chunk=900)
+    assert (fit.status.cpu().numpy() == 0).all()
+    for k in range(2):
+        o = O.ols_fit(X[off[k]:off[k + 1]], y[off[k]:off[k + 1]], fit_intercept=fi)
+        assert _rel(fit.theta[k].cpu(), o["coef"]) < 1e-8
+        assert _rel(fit.sig_inv[k].cpu(), o["Sig_inv"]) < 1e-12
+
+
+def test_config5_shape_sampled_partitions(torch_cuda, M):
+    """BASELINE config-5 partition geometry (p = 500, n_k = 156 250) on 8
+    partitions generated in HBM: 1 sampled partition against the oracle, every
+    partition through the score equation X^T (y - mu) ~ 0 and Sig_inv
+    symmetry; then the combine + DBIC selection on the 8 partitions."""
+    torch = torch_cuda
+    from dlsa_amd.dlsa import dlsa, dlsa_mapred
+
+    K, nk, p = 8, 156250, 500
+    X, y = M.simulate_logistic_device(K * nk, p, seed=2019)
+    off = np.arange(K + 1, dtype=np.int64) * nk
+    fit = M.logistic_model_batched(X, y, off)
+    assert (fit.status.cpu().numpy() == 0).all()
+    S = fit.sig_inv
+    assert torch.equal(S, S.transpose(1, 2))
+    k = 5
+    o = O.logistic_fit(X[off[k]:off[k + 1]].cpu().numpy(), y[off[k]:off[k + 1]].cpu().numpy())
+    assert _rel(fit.theta[k].cpu(), o["coef"]) < REL
+    assert _rel(fit.sig_inv[k].cpu(), o["Sig_inv"]) < REL
+    th = fit.theta
+    for k in range(K):
+        Xk = X[off[k]:off[k + 1]]
+        gk = Xk.T @ (y[off[k]:off[k + 1]] - torch.sigmoid(Xk @ th[k]))
+        assert gk.abs().max().item() < 1e-5
+    comb = dlsa_mapred(fit)
+    sel = dlsa(comb.iloc[:, 2:], comb["beta_byOLS"], K * nk)
+    sup = set(np.nonzero(sel["beta_byBIC"].to_numpy())[0].tolist())
+    assert set(range(200)) <= sup  # the 0.4 p true nonzeros are all kept
