@@ -45,18 +45,34 @@ static bool use_perwave_pass() {
   return e && strcmp(e, "perwave") == 0;
 }
 
-static int auto_rows_per_chunk(int64_t n_total) {
+// Pass kernel of a precision phase: the register-streaming pass (one wave
+// per chunk, all tiles in registers; P <= 112) or the cooperative LDS pass.
+// DLSA_PASS_F64 / DLSA_PASS_LOWP = reg | coop override the default.
+static bool use_reg_pass(int NT, bool f64) {
+  if (NT > kRegMaxNT || use_perwave_pass()) return false;
+  const char* e = getenv(f64 ? "DLSA_PASS_F64" : "DLSA_PASS_LOWP");
+  if (e) return strcmp(e, "reg") == 0;
+  return false;
+}
+
+static int auto_rows_per_chunk(int64_t n_total, int NT = 0) {
   if (const char* e = getenv("DLSA_ROWS_PER_CHUNK")) return std::max(64, atoi(e));
+  if (NT > 0 && (use_reg_pass(NT, true) || use_reg_pass(NT, false))) {
+    // one wave per chunk: ~4 rounds of 4 waves per CU on 256 CUs
+    int64_t r = n_total / 4096;
+    return (int)std::max<int64_t>(1024, std::min<int64_t>(r, 65536));
+  }
   if (use_perwave_pass()) {
     // one wave per chunk: ~8 waves per CU-slot round on 256 CUs
     int64_t r = n_total / 4096;
     r = std::max<int64_t>(256, std::min<int64_t>(r, 8192));
     return (int)r;
   }
-  // one 4-wave workgroup per chunk: ~4 rounds of 256 workgroups, so a
-  // partition of ~1e5 rows is one chunk at config 2 and small fits still
-  // spread over the CUs
-  int64_t r = n_total / 1024;
+  // one 4-wave workgroup per chunk, ~8192 chunks: measured at config 2
+  // (bf16 / fp64 pass ms) 1024 chunks 22.0 / 42.5, 2048 19.4 / 36.6,
+  // 4096 18.2 / 34.7, 8192 17.4 / 33.2, 16384 17.0 / 32.8 (but the Newton
+  // solve reads every chunk's partial tiles: 0.65 -> 0.74 ms per iteration)
+  int64_t r = n_total / 8192;
   r = std::max<int64_t>(1024, std::min<int64_t>(r, 131072));
   return (int)r;
 }
@@ -70,7 +86,7 @@ static bool make_plan(const int64_t* offsets, int K, int p, int intercept, int r
   pl.T = pl.NT * (pl.NT + 1) / 2;
   pl.PP = 16 * pl.NT;
   const int64_t n_total = offsets[K];
-  const int rpc = rows_per_chunk > 0 ? rows_per_chunk : auto_rows_per_chunk(n_total);
+  const int rpc = rows_per_chunk > 0 ? rows_per_chunk : auto_rows_per_chunk(n_total, pl.NT);
   pl.part_chunk_begin.assign(K + 1, 0);
   pl.chunk_row0.clear();
   pl.chunk_rows.clear();
@@ -394,9 +410,10 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
   }
   plans.push_back(fin);
 
-  // the Gram pass has an fp64 MFMA variant only: every wide fit runs its
-  // Newton passes with the fp64 Hessian
-  const int start_phase = PHASE_F64;
+  // MIXED / MIXED_F32: bf16-MFMA Gram passes until the step is below
+  // switch_tol, then fp64 Gram passes (the fused path's phase machine)
+  const int start_phase =
+      (opt.hessian_mode == DLSA_HESSIAN_FP64 || family == FAMILY_GAUSSIAN) ? PHASE_F64 : PHASE_F32;
   DLSA_HIP_TRY(launch_fit_init(d_offsets, K, P, start_phase, theta, d_phase, d_bt, iters, status,
                                d_llprev, sig_inv, loglik, stream));
   int n_running[2] = {0, 0};
@@ -456,25 +473,29 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
     sa.switch_tol = final_level ? opt.switch_tol : 0.0;
     const int it_end = final_level ? max_iter : std::min(max_iter, it + 10);
     for (; it < it_end && (n_running[0] + n_running[1]) > 0 && q.rows.n_chunks > 0; ++it) {
-      double ms_row = 0.0, ms_gram = 0.0;
+      double ms_row = 0.0;
       DLSA_HIP_TRY(timed(&ms_row, [&] {
         return launch_wide_row(wa, standardize, family, q.rows.n_chunks, stream);
       }));
+      g_stats.ms_wide_row += ms_row;
       for (int ph = 0; ph < 2; ++ph) {
         if (n_running[ph] == 0) continue;
         wa.want_phase = ph;
-        DLSA_HIP_TRY(timed(&ms_gram, [&] { return launch_wide_gram(wa, standardize, stream); }));
+        double ms_gram = 0.0;
+        DLSA_HIP_TRY(timed(&ms_gram, [&] {
+          return launch_wide_gram(wa, standardize, ph == PHASE_F64, stream);
+        }));
+        g_stats.ms_wide_gram += ms_gram;
         if (ph == PHASE_F64) {
           g_stats.passes_fp64++;
           g_stats.rows_fp64 += rows;
+          g_stats.ms_pass_fp64 += ms_gram;
         } else {
           g_stats.passes_fp32++;
           g_stats.rows_fp32 += rows;
+          g_stats.ms_pass_fp32 += ms_gram;
         }
       }
-      g_stats.ms_wide_row += ms_row;
-      g_stats.ms_wide_gram += ms_gram;
-      g_stats.ms_pass_fp64 += ms_row + ms_gram;
       DLSA_HIP_TRY(timed(&g_stats.ms_wide_assemble,
                          [&] { return launch_wide_assemble(wa, d_gcb, d_H, K, stream); }));
       DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
@@ -744,6 +765,7 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
       if (n_running[ph] == 0) continue;
       const bool f64 = ph == PHASE_F64;
       pa.want_phase = ph;
+      const bool reg = use_reg_pass(q.NT, f64);
       int nslot;
       if (perwave) {
         int waves = pass_waves_per_cu(f64);
@@ -751,10 +773,10 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
         nslot = (160 * 1024 / std::max(waves, 1)) / pa.slot_bytes;
         nslot = std::max(2, std::min(nslot, 4));
       } else {
-        // bf16/fp32 passes: one workgroup per CU with a deep ring (HBM-bound);
-        // fp64 passes: two workgroups per CU so one's VALU row phase overlaps
-        // the other's MFMA tile phase (MFMA-bound)
-        int wg_per_cu = (f64 && pl.NT < 8) ? 2 : 1;
+        // two workgroups per CU (P <= 112): one's row phase and barrier waits
+        // overlap the other's tile phase (measured 27.4 -> 21.8 ms per bf16
+        // pass at config 2 against one workgroup with a deeper ring)
+        int wg_per_cu = pl.NT < 8 ? 2 : 1;
         if (const char* e = getenv(f64 ? "DLSA_WG_F64" : "DLSA_WG_LOWP")) wg_per_cu = atoi(e);
         const int budget =
             160 * 1024 / std::max(wg_per_cu, 1) - coop_extra_bytes(pl.NT);
@@ -763,6 +785,7 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
       if (const char* e = getenv("DLSA_NSLOT")) nslot = std::max(2, std::min(atoi(e), perwave ? 4 : 6));
       pa.nslot = nslot;
       DLSA_HIP_TRY(timed(f64 ? &g_stats.ms_pass_fp64 : &g_stats.ms_pass_fp32, [&] {
+        if (reg) return launch_irls_reg(pa, q.NT, f64, standardize, family, q.n_chunks, stream);
         if (perwave)
           return launch_irls_pass(pa, q.NT, f64, standardize, family, q.n_chunks, stream);
         return launch_irls_coop(pa, q.NT, f64 ? PREC_F64 : approx_prec, standardize, family,

@@ -123,7 +123,7 @@ struct WideArgs {
 // Launchers (defined in the .hip files).
 hipError_t launch_wide_row(const WideArgs& a, bool standardize, int family, int n_chunks,
                            hipStream_t s);
-hipError_t launch_wide_gram(const WideArgs& a, bool standardize, hipStream_t s);
+hipError_t launch_wide_gram(const WideArgs& a, bool standardize, bool f64, hipStream_t s);
 hipError_t launch_wide_assemble(const WideArgs& a, const int32_t* gcb, double* Hfull, int K,
                                 hipStream_t s);
 hipError_t launch_wide_newton(const SolveArgs& sa, const WideArgs& wa, const int32_t* rcb,
@@ -133,6 +133,9 @@ hipError_t launch_loglik_eval(const EvalArgs& a, int n_chunks, hipStream_t s);
 hipError_t launch_loglik_reduce(const double* partial, const int32_t* pcb, int K, int B,
                                 double* out, hipStream_t s);
 int eval_slot_bytes(int p);
+hipError_t launch_irls_reg(const PassArgs& a, int NT, bool f64, bool standardize, int family,
+                           int n_chunks, hipStream_t s);
+constexpr int kRegMaxNT = 7;  // register-streaming pass: fp64 accumulators of all tiles in one wave
 hipError_t launch_irls_pass(const PassArgs& a, int NT, bool f64, bool standardize,
                             int family, int n_chunks, hipStream_t s);
 int pass_slot_bytes(int NT);

@@ -246,7 +246,7 @@ __device__ __forceinline__ void store_tiles(Acc (&acc)[(CG<NT, W>::TPW)], double
 }
 
 template <int NT, int W, int PREC, bool STD, int FAM>
-__global__ __launch_bounds__(64 * W, (W == 8 || (PREC == PREC_F64 && NT < 8)) ? 2 : 1)
+__global__ __launch_bounds__(64 * W, (W == 8 || NT < 8) ? 2 : 1)
 void irls_coop_kernel(const PassArgs a) {
   using G = CG<NT, W>;
   using Acc = typename std::conditional<PREC == PREC_F64, d4, f4>::type;

@@ -290,6 +290,156 @@ __global__ __launch_bounds__(512, 1) void wide_gram_kernel(const WideArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// approximate Gram pass (bf16 MFMA, fp32 accumulation) for the Newton steps
+// before the fp64 pass (the approximate Hessian only steers
+// Newton; the fp64 gradient fixes the solution).  Same (row group, tile)
+// grid and XCD mapping as wide_gram_kernel.  Per 32-row block the 512
+// threads stage the tile's two 128-feature column blocks through LDS:
+// thread (feature f = t & 127, row octet g = t >> 7) loads rows 8g .. 8g+7
+// of feature f (each load instruction = 64 consecutive features of one row,
+// 512 contiguous bytes), converts to bf16 (A image: w x, B image: x) and
+// writes the 8 rows as ONE 16-byte LDS store -- exactly the k-contiguous
+// operand of v_mfma_f32_16x16x32_bf16 (lane (i, kg) reads feature i, rows
+// 8 kg .. 8 kg + 7 with one ds_read_b128).  Feature stride 80 B: the 16
+// lanes of an operand read hit 16 distinct 16-byte bank groups.
+// Double-buffered images: one barrier per block.
+// ---------------------------------------------------------------------------
+typedef __bf16 bf16x8w __attribute__((ext_vector_type(8)));
+typedef float f4w __attribute__((ext_vector_type(4)));
+
+namespace {
+constexpr int IMG_STRIDE = 80;                       // bytes per feature row of an image
+constexpr int IMG_BYTES = GT * IMG_STRIDE;           // one 128-feature x 32-row image
+}  // namespace
+
+template <bool STD>
+__global__ __launch_bounds__(512, 1) void wide_gram_bf16_kernel(const WideArgs a) {
+  __shared__ __attribute__((aligned(16))) char img[2][2][IMG_BYTES];  // [buf][A | B]
+  const int NB = a.NB;
+  const int TB = NB * (NB + 1) / 2;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, j8 = bid >> 3;
+  const int cl = j8 / TB, t = j8 - cl * TB;
+  const int chunk = cl * 8 + xcd;
+  if (chunk >= a.n_gchunks) return;
+  const int part = a.gc_part[chunk];
+  if (a.phase[part] != a.want_phase) return;  // workgroup-uniform
+  int I, J;
+  tile_ij(t, I, J);
+  const bool diag = I == J;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int qi = wid >> 1, qj = wid & 1;
+  const bool mma = !(diag && qj == 1 && qi < 2);  // wave-uniform
+  const int p = a.p, ic = a.intercept;
+  const int64_t row0 = a.gc_row0[chunk];
+  const int nrows = a.gc_rows[chunk];
+  const int nb = (nrows + 31) / 32;
+
+  // staging role: feature fs of both column blocks, rows 8 g .. 8 g + 7
+  const int fs = tid & 127, g = tid >> 7;
+  auto feat = [&](int blk, int& col, bool& in, bool& one, double& c, double& s) {
+    const int f = GT * blk + fs, jj = f - ic;
+    in = jj >= 0 && jj < p;
+    one = ic && f == 0;
+    col = in ? jj : 0;
+    c = 0.0;
+    s = 1.0;
+    if constexpr (STD) {
+      if (in) {
+        c = a.center[jj];
+        s = 1.0 / a.scale[jj];
+      }
+    }
+  };
+  int colI, colJ;
+  bool inI, inJ, oneI, oneJ;
+  double cI, sI, cJ, sJ;
+  feat(I, colI, inI, oneI, cI, sI);
+  feat(J, colJ, inJ, oneJ, cJ, sJ);
+
+  double xi[8], xj[8], wv[8];
+  auto load = [&](int b) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int r = 32 * b + 8 * g + e;
+      const bool valid = r < nrows;
+      const int rc = valid ? r : nrows - 1;
+      const double* xr = a.X + (row0 + rc) * (int64_t)p;
+      wv[e] = valid ? a.w[row0 + rc] : 0.0;
+      xi[e] = xr[colI];
+      if (!diag) xj[e] = xr[colJ];
+    }
+  };
+  auto stage = [&](int buf) {
+    bf16x8w va, vb;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      double v = inI ? xi[e] : 0.0;
+      if constexpr (STD) v = (v - cI) * sI;
+      if (oneI) v = 1.0;
+      va[e] = (__bf16)(float)(v * wv[e]);
+      double u = v;
+      if (!diag) {
+        u = inJ ? xj[e] : 0.0;
+        if constexpr (STD) u = (u - cJ) * sJ;
+        if (oneJ) u = 1.0;
+      }
+      vb[e] = (__bf16)(float)u;
+    }
+    *(bf16x8w*)(img[buf][0] + fs * IMG_STRIDE + 16 * g) = va;
+    *(bf16x8w*)(img[buf][1] + fs * IMG_STRIDE + 16 * g) = vb;
+  };
+
+  f4w acc[2][4];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[s][b] = f4w{0.f, 0.f, 0.f, 0.f};
+  const int fl = lane & 15, kg = lane >> 4;
+
+  if (nb > 0) {
+    load(0);
+    stage(0);
+  }
+  for (int b = 0; b < nb; ++b) {
+    if (b + 1 < nb) load(b + 1);  // in flight during the barrier and the MFMAs
+    __syncthreads();              // image b % 2 complete; image (b+1) % 2 free
+    if (mma) {
+      const char* A = img[b & 1][0];
+      const char* B = img[b & 1][1];
+      bf16x8w av[2], bv[4];
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        av[s] = *(const bf16x8w*)(A + (32 * qi + 16 * s + fl) * IMG_STRIDE + 16 * kg);
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        bv[c] = *(const bf16x8w*)(B + (64 * qj + 16 * c + fl) * IMG_STRIDE + 16 * kg);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          acc[s][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[s], bv[c], acc[s][c], 0, 0, 0);
+    }
+    if (b + 1 < nb) stage((b + 1) & 1);
+  }
+
+  if (!mma) return;
+  // C/D map of the f32 16x16 MFMAs: row = 4 (l >> 4) + r, column = l & 15
+  double* G = a.slab_G + ((int64_t)chunk * TB + t) * (GT * GT);
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 32 * qi + 16 * s + 4 * kg + r;
+        const int jc = 64 * qj + 16 * c + fl;
+        G[i * GT + jc] = (double)acc[s][c][r];
+      }
+}
+
+// ---------------------------------------------------------------------------
 // assemble: H[k] (PP x PP, both triangles, padding = identity) = sum of the
 // row-group partials of partition k in row-group order.  grid (TB, K).
 // ---------------------------------------------------------------------------
@@ -661,10 +811,17 @@ hipError_t launch_wide_row(const WideArgs& a, bool standardize, int family, int 
   }
 }
 
-hipError_t launch_wide_gram(const WideArgs& a, bool standardize, hipStream_t s) {
+hipError_t launch_wide_gram(const WideArgs& a, bool standardize, bool f64, hipStream_t s) {
   if (a.n_gchunks <= 0) return hipSuccess;
   const int TB = a.NB * (a.NB + 1) / 2;
   const int grid = ((a.n_gchunks + 7) / 8) * 8 * TB;
+  if (!f64) {
+    if (standardize)
+      hipLaunchKernelGGL(wide_gram_bf16_kernel<true>, dim3(grid), dim3(512), 0, s, a);
+    else
+      hipLaunchKernelGGL(wide_gram_bf16_kernel<false>, dim3(grid), dim3(512), 0, s, a);
+    return hipGetLastError();
+  }
   if (standardize)
     hipLaunchKernelGGL(wide_gram_kernel<true>, dim3(grid), dim3(512), 0, s, a);
   else

@@ -101,8 +101,8 @@ typedef struct dlsa_fit_stats {
   int64_t rows_fp32;        /* rows streamed by approximate-Hessian passes (sum
                                over launches, warm-start levels included) */
   int64_t rows_fp64;        /* rows streamed by fp64 passes (sum) */
-  double ms_wide_row;       /* P > DLSA_MAX_P_FUSED: row-pass kernel time (included
-                               in ms_pass_fp32/fp64 with the Gram pass) */
+  double ms_wide_row;       /* P > DLSA_MAX_P_FUSED: row-pass kernel time (there
+                               ms_pass_fp32/fp64 hold the bf16 / fp64 Gram-pass time) */
   double ms_wide_gram;      /* P > DLSA_MAX_P_FUSED: Gram-pass kernel time */
   double ms_wide_assemble;  /* P > DLSA_MAX_P_FUSED: partial-tile assembly time */
 } dlsa_fit_stats;
