@@ -55,6 +55,15 @@ static bool use_reg_pass(int NT, bool f64) {
   return false;
 }
 
+// fp64 passes: the wave-specialised kernel (P <= 128) unless
+// DLSA_PASS_F64 = coop | reg
+static bool use_ws_pass(int NT) {
+  if (NT > kWsMaxNT || use_perwave_pass()) return false;
+  const char* e = getenv("DLSA_PASS_F64");
+  if (e) return strcmp(e, "ws") == 0;
+  return false;
+}
+
 static int auto_rows_per_chunk(int64_t n_total, int NT = 0) {
   if (const char* e = getenv("DLSA_ROWS_PER_CHUNK")) return std::max(64, atoi(e));
   if (NT > 0 && (use_reg_pass(NT, true) || use_reg_pass(NT, false))) {
@@ -766,8 +775,11 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
       const bool f64 = ph == PHASE_F64;
       pa.want_phase = ph;
       const bool reg = use_reg_pass(q.NT, f64);
+      const bool ws = f64 && !reg && use_ws_pass(q.NT);
       int nslot;
-      if (perwave) {
+      if (ws) {
+        nslot = ws_nslot(q.NT, p);
+      } else if (perwave) {
         int waves = pass_waves_per_cu(f64);
         if (const char* e = getenv(f64 ? "DLSA_WAVES_F64" : "DLSA_WAVES_F32")) waves = atoi(e);
         nslot = (160 * 1024 / std::max(waves, 1)) / pa.slot_bytes;
@@ -782,10 +794,14 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
             160 * 1024 / std::max(wg_per_cu, 1) - coop_extra_bytes(pl.NT);
         nslot = std::max(2, std::min(budget / pa.slot_bytes, 6));
       }
-      if (const char* e = getenv("DLSA_NSLOT")) nslot = std::max(2, std::min(atoi(e), perwave ? 4 : 6));
+      if (const char* e = getenv("DLSA_NSLOT"))
+        nslot = std::max(ws ? 3 : 2, std::min(atoi(e), perwave ? 4 : (ws ? 5 : 6)));
       pa.nslot = nslot;
+      pa.slot_bytes = ws ? ws_slot_bytes(q.NT, p)
+                         : (perwave ? pass_slot_bytes(q.NT) : coop_slot_bytes(q.NT, p));
       DLSA_HIP_TRY(timed(f64 ? &g_stats.ms_pass_fp64 : &g_stats.ms_pass_fp32, [&] {
         if (reg) return launch_irls_reg(pa, q.NT, f64, standardize, family, q.n_chunks, stream);
+        if (ws) return launch_irls_ws(pa, q.NT, standardize, family, q.n_chunks, stream);
         if (perwave)
           return launch_irls_pass(pa, q.NT, f64, standardize, family, q.n_chunks, stream);
         return launch_irls_coop(pa, q.NT, f64 ? PREC_F64 : approx_prec, standardize, family,

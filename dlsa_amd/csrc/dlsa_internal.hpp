@@ -135,7 +135,13 @@ hipError_t launch_loglik_reduce(const double* partial, const int32_t* pcb, int K
 int eval_slot_bytes(int p);
 hipError_t launch_irls_reg(const PassArgs& a, int NT, bool f64, bool standardize, int family,
                            int n_chunks, hipStream_t s);
-constexpr int kRegMaxNT = 7;  // register-streaming pass: fp64 accumulators of all tiles in one wave
+constexpr int kRegMaxNT = 7;
+// wave-specialised fp64 pass (irls_ws_impl.hpp): P <= 128
+hipError_t launch_irls_ws(const PassArgs& a, int NT, bool standardize, int family, int n_chunks,
+                          hipStream_t s);
+int ws_slot_bytes(int NT, int p);  // one producer sub-slot
+int ws_nslot(int NT, int p);
+constexpr int kWsMaxNT = 8;  // register-streaming pass: fp64 accumulators of all tiles in one wave
 hipError_t launch_irls_pass(const PassArgs& a, int NT, bool f64, bool standardize,
                             int family, int n_chunks, hipStream_t s);
 int pass_slot_bytes(int NT);

@@ -38,6 +38,8 @@ namespace dlsa {
 typedef double d4 __attribute__((ext_vector_type(4)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2c __attribute__((ext_vector_type(2)));
+typedef float f2c __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef const __attribute__((address_space(1))) void gbl_void_t;
 
@@ -111,6 +113,8 @@ struct CG {
   static constexpr int TPW = (T + W - 1) / W;  // tiles per wave (contiguous ranges)
   static constexpr int M = PMAX / LPR;         // features per lane in the row phase
   static constexpr int PAD = 16;
+  static constexpr int OBS = RB + 8;            // bf16 image: elements per feature row (80 B:
+                                               // conflict-free 16-B operand reads)
   static constexpr int MAX_PIECES = (RB * PMAX * 8 + 16 + 1023) / 1024;
   static constexpr int MAX_D = (MAX_PIECES + W - 1) / W;  // DMA pieces per wave per block
   // tiles of wave `wid`: t in [wid*TPW, min(T, (wid+1)*TPW))
@@ -158,10 +162,10 @@ inline int coop_slot_bytes_impl(int NT, int p) {
 
 // LDS beyond the ring: w, r of the block [2][RB] fp64, center / 1/scale
 // [2][PMAX] fp64, and the bf16 MFMA operands of the block: x and w*x,
-// [PMAX][RB] bf16 each (feature-major, so one lane's 8 consecutive k are one
+// [PMAX][RB + 8] bf16 each (feature-major, so one lane's 8 consecutive k are one
 // 16-byte read).
 inline int coop_extra_bytes_impl(int NT) {
-  return (2 * RB + 2 * 16 * NT) * 8 + 2 * 16 * NT * RB * 2;
+  return (2 * RB + 2 * 16 * NT) * 8 + 2 * 16 * NT * (RB + 8) * 2;
 }
 
 // Tile phase of wave WID for one 32-row block.
@@ -177,12 +181,12 @@ __device__ __forceinline__ void tile_phase(Acc (&acc)[(CG<NT, W>::TPW)], const d
   const double* xq = xs + q * p + (fl - ic);  // row q of the block, this lane's feature
   if constexpr (PREC == PREC_BF16) {
     // operands staged by the row phase: k index 8q + j = block row 8q + j
-    const __bf16* obw = obx + G::PMAX * RB;
+    const __bf16* obw = obx + G::PMAX * G::OBS;
     bf16x8 Bv[NT], Av[NT];
     static_for<NT>([&](auto cI) {
       constexpr int c = decltype(cI)::value;
       if constexpr ((CM >> c) & 1u) {
-        const int o = (16 * c + fl) * RB + 8 * q;
+        const int o = (16 * c + fl) * G::OBS + 8 * q;
         Bv[c] = *(const bf16x8*)(obx + o);
         if constexpr ((RM >> c) & 1u) Av[c] = *(const bf16x8*)(obw + o);
       }
@@ -273,11 +277,15 @@ void irls_coop_kernel(const PassArgs a) {
   const int slot_x = G::PAD + d * W * 1024 + G::PMAX * 8;  // y follows
   double* wr = (double*)(smem + nslot * slot_bytes);       // [2][RB]: w, r of the block
   double* stdv = wr + 2 * RB;  // [2][PMAX]: center, 1/scale by feature (STD only)
-  __bf16* obx = (__bf16*)(stdv + 2 * G::PMAX);  // [2][PMAX][RB] bf16 operands (PREC_BF16)
+  __bf16* obx = (__bf16*)(stdv + 2 * G::PMAX);  // [2][PMAX][OBS] bf16 operands (PREC_BF16)
 
-  // ---- row-phase constants: lane handles features f = sl + 8m ------------
-  const int sl = lane % LPR;
-  const int rB = wid * RPW + lane / LPR;  // block row of this lane in the row phase
+  // ---- row-phase constants: lane = (feature group sl, row lane % RPW);
+  // lane handles features f = sl + LPR m of its row.  Row-major ring reads of
+  // one instruction cover RPW rows x LPR consecutive doubles per half-wave
+  // (conflict-free at p = 100), and one feature's RPW rows are written to the
+  // bf16 image by RPW consecutive lanes.
+  const int sl = lane / RPW;
+  const int rB = wid * RPW + lane % RPW;  // block row of this lane in the row phase
   double beta[M], gacc[M];
 #pragma unroll
   for (int m = 0; m < M; ++m) {
@@ -286,6 +294,15 @@ void irls_coop_kernel(const PassArgs a) {
     gacc[m] = 0.0;
   }
   double llacc = 0.0;
+  int tI[G::TPW], tJ[G::TPW];  // this wave's tiles (bf16 path)
+#pragma unroll
+  for (int i = 0; i < G::TPW; ++i) {
+    const int t = wid * G::TPW + i;
+    int I = 0;
+    while ((I + 1) * (I + 2) / 2 <= t) ++I;
+    tI[i] = __builtin_amdgcn_readfirstlane(I);
+    tJ[i] = __builtin_amdgcn_readfirstlane(t - I * (I + 1) / 2);
+  }
   Acc acc[G::TPW];
 #pragma unroll
   for (int i = 0; i < G::TPW; ++i) acc[i] = Acc{0, 0, 0, 0};
@@ -303,22 +320,31 @@ void irls_coop_kernel(const PassArgs a) {
   }
   __syncthreads();
 
+  // Buffer resources over this chunk's rows (bounds-checked raw buffers: a
+  // tail piece past the end of X reads zeros instead of faulting), so a DMA
+  // piece is one buffer_load ... lds with a scalar offset -- no per-lane
+  // 64-bit address arithmetic.
+  const uintptr_t xcb = (uintptr_t)(a.X + row0 * p) & ~(uintptr_t)15;
+  const uintptr_t xend = a.x_last16 + 16;
+  const __amdgpu_buffer_rsrc_t xr_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)xcb, (short)0, (int)min<uintptr_t>(xend - xcb, 0x7FFFFFF0u), 0x00020000);
+  const uintptr_t ycb = (uintptr_t)(a.y + row0);
+  const __amdgpu_buffer_rsrc_t yr_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)ycb, (short)0, (int)min<uintptr_t>(a.y_last4 + 4 - ycb, 0x7FFFFFF0u), 0x00020000);
+  const int vx = lane * 16, vy = lane * 4;
   auto issue = [&](int blk) {
     const int bb = blk < nb ? blk : nb - 1;  // tail: harmless re-fetch, fixed counts
     char* sbase = smem + (blk % nslot) * slot_bytes;
     const uintptr_t start = (uintptr_t)(a.X + (row0 + (int64_t)bb * RB) * p);
-    const uintptr_t al = start & ~(uintptr_t)15;
+    const int so = (int)((start & ~(uintptr_t)15) - xcb);
     for (int i = 0; i < d; ++i) {
       int j = wid + W * i;
       const int jj = j < npieces ? j : npieces - 1;
-      uintptr_t src = al + (uintptr_t)jj * 1024 + (uintptr_t)lane * 16;
-      src = src < a.x_last16 ? src : a.x_last16;
-      __builtin_amdgcn_global_load_lds((gbl_void_t*)src,
-                                       (lds_void_t*)(sbase + G::PAD + j * 1024), 16, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          xr_rsrc, (lds_void_t*)(sbase + G::PAD + j * 1024), 16, vx, so + jj * 1024, 0, 0);
     }
-    uintptr_t ys = (uintptr_t)(a.y + row0 + (int64_t)bb * RB) + (uintptr_t)lane * 4;
-    ys = ys < a.y_last4 ? ys : a.y_last4;
-    __builtin_amdgcn_global_load_lds((gbl_void_t*)ys, (lds_void_t*)(sbase + slot_x), 4, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(yr_rsrc, (lds_void_t*)(sbase + slot_x), 4, vy,
+                                             bb * RB * 8, 0, 0);
   };
 
   for (int b = 0; b < nslot - 1; ++b) issue(b);
@@ -349,7 +375,8 @@ void irls_coop_kernel(const PassArgs a) {
         xv[m] = v;
         e = fma(v, beta[m], e);
       }
-      e = red_row<LPR>(e);
+#pragma unroll
+      for (int o = RPW; o < 64; o <<= 1) e += __shfl_xor(e, o);  // bitwise-identical in all lanes
       const double yv = ys[rB];
       double w, r;
       if constexpr (FAM == FAMILY_LOGISTIC && DLSA_ABLATE == 2) {
@@ -388,21 +415,46 @@ void irls_coop_kernel(const PassArgs a) {
         const float wf = (float)w;
 #pragma unroll
         for (int m = 0; m < M; ++m) {
-          const int o = (sl + LPR * m) * RB + rB;
-          const float xf = (float)xv[m];
-          obx[o] = (__bf16)xf;
-          obx[G::PMAX * RB + o] = (__bf16)(xf * wf);
+          const int o = (sl + LPR * m) * G::OBS + rB;
+          float xf = (float)xv[m];
+          // opaque to the optimiser: otherwise (bf16)(float)x is folded into a
+          // direct f64 -> bf16 conversion, lowered with round-to-odd fix-ups
+          // (6 extra VALU per value); x is finite, double rounding is harmless
+          asm volatile("" : "+v"(xf));
+          // one v_cvt_pk_bf16_f32 for x and w x; halves stored with
+          // ds_write_b16 / ds_write_b16_d16_hi
+          const f2c pr = {xf, xf * wf};
+          const bf16x2c pk = __builtin_convertvector(pr, bf16x2c);
+          obx[o] = pk[0];
+          obx[G::PMAX * G::OBS + o] = pk[1];
         }
       }
     }
     __syncthreads();  // B2: w, r of all 32 rows visible
 
     // ---- C: tile phase -----------------------------------------------------
-    if constexpr (DLSA_ABLATE != 1 && DLSA_ABLATE != 3)
-    static_for<W>([&](auto wI) {
-      constexpr int WID = decltype(wI)::value;
-      if (wid == WID) tile_phase<NT, W, PREC, STD, WID>(acc, xs, wr, p, ic, lane, stdv, obx);
-    });
+    if constexpr (DLSA_ABLATE != 1 && DLSA_ABLATE != 3) {
+      if constexpr (PREC == PREC_BF16) {
+        // one code path for every wave: the wave's tile indices are
+        // wave-uniform registers (no per-wave copies of the loop body, whose
+        // merge would copy the accumulators every block)
+        const __bf16* obw = obx + G::PMAX * G::OBS;
+        const int fl = lane & 15, q = lane >> 4;
+#pragma unroll
+        for (int i = 0; i < G::TPW; ++i) {
+          if (wid * G::TPW + i < G::T) {  // wave-uniform
+            const bf16x8 Av = *(const bf16x8*)(obw + (16 * tI[i] + fl) * G::OBS + 8 * q);
+            const bf16x8 Bv = *(const bf16x8*)(obx + (16 * tJ[i] + fl) * G::OBS + 8 * q);
+            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Av, Bv, acc[i], 0, 0, 0);
+          }
+        }
+      } else {
+        static_for<W>([&](auto wI) {
+          constexpr int WID = decltype(wI)::value;
+          if (wid == WID) tile_phase<NT, W, PREC, STD, WID>(acc, xs, wr, p, ic, lane, stdv, obx);
+        });
+      }
+    }
   }
   wait_vmcnt<0>();  // drain the tail re-fetches
   __syncthreads();
@@ -413,17 +465,17 @@ void irls_coop_kernel(const PassArgs a) {
     constexpr int WID = decltype(wI)::value;
     if (wid == WID) store_tiles<NT, W, PREC, STD, WID>(acc, sH, lane);
   });
-  // gradient: sum the row-lanes of each feature (xor LPR .. 32), then the waves
+  // gradient: sum the row lanes of each feature group (xor 1 .. RPW/2), then the waves
   double* red = (double*)smem;  // ring is no longer needed: [W][PMAX] + [W]
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     double v = gacc[m];
 #pragma unroll
-    for (int o = LPR; o < 64; o <<= 1) v += __shfl_xor(v, o);
-    if (lane < LPR) red[wid * G::PMAX + sl + LPR * m] = v;
+    for (int o = 1; o < RPW; o <<= 1) v += __shfl_xor(v, o);
+    if (lane % RPW == 0) red[wid * G::PMAX + sl + LPR * m] = v;
   }
 #pragma unroll
-  for (int o = LPR; o < 64; o <<= 1) llacc += __shfl_xor(llacc, o);
+  for (int o = 1; o < 64; o <<= 1) llacc += __shfl_xor(llacc, o);
   if (lane == 0) red[W * G::PMAX + wid] = llacc;
   __syncthreads();
   for (int f = tid; f < G::PMAX; f += 64 * W) {

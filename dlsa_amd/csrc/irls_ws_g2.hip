@@ -1,0 +1,16 @@
+// Instantiations of the wave-specialised fp64 pass for NT in {6, 7, 8}.
+#include "irls_ws_impl.hpp"
+
+namespace dlsa {
+
+hipError_t launch_irls_ws_g2(const PassArgs& a, int NT, bool std_, int family, int n_chunks,
+                              hipStream_t s) {
+  switch (NT) {
+    case 6: return launch_ws_nt<6>(a, std_, family, n_chunks, s);
+    case 7: return launch_ws_nt<7>(a, std_, family, n_chunks, s);
+    case 8: return launch_ws_nt<8>(a, std_, family, n_chunks, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace dlsa
