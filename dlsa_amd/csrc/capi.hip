@@ -64,6 +64,15 @@ static bool use_ws_pass(int NT) {
   return false;
 }
 
+// bf16 approximate passes: the light-weight kernel when its in-place operand
+// images fit (P <= 128, P <~ 2p), unless DLSA_PASS_LOWP = coop | reg
+static bool use_lite_pass(int NT, int p, int prec) {
+  if (prec != PREC_BF16 || !lite_fits(NT, p) || use_perwave_pass()) return false;
+  const char* e = getenv("DLSA_PASS_LOWP");
+  if (e) return strcmp(e, "lite") == 0;
+  return false;
+}
+
 static int auto_rows_per_chunk(int64_t n_total, int NT = 0) {
   if (const char* e = getenv("DLSA_ROWS_PER_CHUNK")) return std::max(64, atoi(e));
   if (NT > 0 && (use_reg_pass(NT, true) || use_reg_pass(NT, false))) {
@@ -780,8 +789,12 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
       pa.want_phase = ph;
       const bool reg = use_reg_pass(q.NT, f64);
       const bool ws = f64 && !reg && use_ws_pass(q.NT);
+      const bool lite =
+          !f64 && !reg && family == FAMILY_LOGISTIC && use_lite_pass(q.NT, p, approx_prec);
       int nslot;
-      if (ws) {
+      if (lite) {
+        nslot = lite_nslot(q.NT, p);
+      } else if (ws) {
         nslot = ws_nslot(q.NT, p);
       } else if (perwave) {
         int waves = pass_waves_per_cu(f64);
@@ -799,13 +812,15 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
         nslot = std::max(2, std::min(budget / pa.slot_bytes, 6));
       }
       if (const char* e = getenv("DLSA_NSLOT"))
-        nslot = std::max(ws ? 3 : 2, std::min(atoi(e), perwave ? 4 : (ws ? 5 : 6)));
+        if (!lite) nslot = std::max(ws ? 3 : 2, std::min(atoi(e), perwave ? 4 : (ws ? 5 : 6)));
       pa.nslot = nslot;
-      pa.slot_bytes = ws ? ws_slot_bytes(q.NT, p)
-                         : (perwave ? pass_slot_bytes(q.NT) : coop_slot_bytes(q.NT, p));
+      pa.slot_bytes = lite ? lite_slot_bytes(q.NT, p)
+                           : ws ? ws_slot_bytes(q.NT, p)
+                                : (perwave ? pass_slot_bytes(q.NT) : coop_slot_bytes(q.NT, p));
       DLSA_HIP_TRY(timed(f64 ? &g_stats.ms_pass_fp64 : &g_stats.ms_pass_fp32, [&] {
         if (reg) return launch_irls_reg(pa, q.NT, f64, standardize, family, q.n_chunks, stream);
         if (ws) return launch_irls_ws(pa, q.NT, standardize, family, q.n_chunks, stream);
+        if (lite) return launch_irls_lite(pa, q.NT, standardize, q.n_chunks, stream);
         if (perwave)
           return launch_irls_pass(pa, q.NT, f64, standardize, family, q.n_chunks, stream);
         return launch_irls_coop(pa, q.NT, f64 ? PREC_F64 : approx_prec, standardize, family,

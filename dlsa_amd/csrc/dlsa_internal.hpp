@@ -141,7 +141,13 @@ hipError_t launch_irls_ws(const PassArgs& a, int NT, bool standardize, int famil
                           hipStream_t s);
 int ws_slot_bytes(int NT, int p);  // one producer sub-slot
 int ws_nslot(int NT, int p);
-constexpr int kWsMaxNT = 8;  // register-streaming pass: fp64 accumulators of all tiles in one wave
+constexpr int kWsMaxNT = 8;
+// light-weight approximate-Hessian (bf16) pass (irls_lite_impl.hpp): P <= 112, P <~ 2p
+hipError_t launch_irls_lite(const PassArgs& a, int NT, bool standardize, int n_chunks,
+                            hipStream_t s);
+bool lite_fits(int NT, int p);
+int lite_slot_bytes(int NT, int p);
+int lite_nslot(int NT, int p);  // register-streaming pass: fp64 accumulators of all tiles in one wave
 hipError_t launch_irls_pass(const PassArgs& a, int NT, bool f64, bool standardize,
                             int family, int n_chunks, hipStream_t s);
 int pass_slot_bytes(int NT);
