@@ -113,8 +113,10 @@ struct CG {
   static constexpr int TPW = (T + W - 1) / W;  // tiles per wave (contiguous ranges)
   static constexpr int M = PMAX / LPR;         // features per lane in the row phase
   static constexpr int PAD = 16;
-  static constexpr int OBS = RB + 8;            // bf16 image: elements per feature row (80 B:
-                                               // conflict-free 16-B operand reads)
+  static constexpr int OBS = RB + 16;           // bf16 image: elements per feature row; 96 B
+                                               // (24 dwords) makes the ds_read_b128 operand
+                                               // reads (lane groups of MI355X_MICROARCH.md
+                                               // "LDS") conflict-free -- 80 B is 2-way
   static constexpr int MAX_PIECES = (RB * PMAX * 8 + 16 + 1023) / 1024;
   static constexpr int MAX_D = (MAX_PIECES + W - 1) / W;  // DMA pieces per wave per block
   // tiles of wave `wid`: t in [wid*TPW, min(T, (wid+1)*TPW))
@@ -153,19 +155,19 @@ inline int coop_waves(int NT) {
   return 4;
 }
 
+// A slot holds exactly the block's pieces: a wave's surplus issues (the piece
+// count is rounded up to the wave count so that every wave waits on the same
+// vmcnt) re-load the last piece onto itself.
 inline int coop_slot_bytes_impl(int NT, int p) {
-  const int W = coop_waves(NT);
-  const int npieces = npieces_for(p);
-  const int d = (npieces + W - 1) / W;
-  return 16 + d * W * 1024 + 16 * NT * 8 + RB * 8;
+  return 16 + npieces_for(p) * 1024 + 16 * NT * 8 + RB * 8;
 }
 
 // LDS beyond the ring: w, r of the block [2][RB] fp64, center / 1/scale
 // [2][PMAX] fp64, and the bf16 MFMA operands of the block: x and w*x,
-// [PMAX][RB + 8] bf16 each (feature-major, so one lane's 8 consecutive k are one
+// [PMAX][RB + 16] bf16 each (feature-major, so one lane's 8 consecutive k are one
 // 16-byte read).
 inline int coop_extra_bytes_impl(int NT) {
-  return (2 * RB + 2 * 16 * NT) * 8 + 2 * 16 * NT * (RB + 8) * 2;
+  return (2 * RB + 2 * 16 * NT) * 8 + 2 * 16 * NT * (RB + 16) * 2;
 }
 
 // Tile phase of wave WID for one 32-row block.
@@ -274,7 +276,7 @@ void irls_coop_kernel(const PassArgs a) {
   const int slot_bytes = a.slot_bytes;
   const int npieces = npieces_for(p);
   const int d = (npieces + W - 1) / W;
-  const int slot_x = G::PAD + d * W * 1024 + G::PMAX * 8;  // y follows
+  const int slot_x = G::PAD + npieces * 1024 + G::PMAX * 8;  // y follows
   double* wr = (double*)(smem + nslot * slot_bytes);       // [2][RB]: w, r of the block
   double* stdv = wr + 2 * RB;  // [2][PMAX]: center, 1/scale by feature (STD only)
   __bf16* obx = (__bf16*)(stdv + 2 * G::PMAX);  // [2][PMAX][OBS] bf16 operands (PREC_BF16)
@@ -341,7 +343,7 @@ void irls_coop_kernel(const PassArgs a) {
       int j = wid + W * i;
       const int jj = j < npieces ? j : npieces - 1;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          xr_rsrc, (lds_void_t*)(sbase + G::PAD + j * 1024), 16, vx, so + jj * 1024, 0, 0);
+          xr_rsrc, (lds_void_t*)(sbase + G::PAD + jj * 1024), 16, vx, so + jj * 1024, 0, 0);
     }
     __builtin_amdgcn_raw_ptr_buffer_load_lds(yr_rsrc, (lds_void_t*)(sbase + slot_x), 4, vy,
                                              bb * RB * 8, 0, 0);
