@@ -83,7 +83,7 @@ typedef struct dlsa_fit_options {
   int32_t warm_start;       /* 1 (default): the first Newton iterations run on
                                row prefixes of each partition (1/16, then 1/4
                                of the rows, never fewer than max(2048, 64 P))
-                               to a 1e-2 step, then on all rows to tol -- the
+                               to a 0.1-relative step, then on all rows to tol -- the
                                fixed point is unchanged; 0: all rows from the
                                start */
   int32_t reserved[6];
