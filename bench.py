@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """DLSA logistic fit benchmark (BASELINE.json metric, config 2 by default).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|4|5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
@@ -14,6 +14,8 @@ before the timed region.
 
 Configs (BASELINE.json "configs"); per GPU (weak scaling):
   2  logistic n = 1e8, p = 100, K = 1024            (default; the headline metric)
+  3  logistic n = 1.5e7, p = 181 + intercept, K = 128 (airline-like dummy-coded design;
+                                                     1.2e8 rows on 8 GPUs)
   5  logistic n = 5e6, p = 500, K = 32              (wide path: row + Gram pass)
   4  OLS      n = 1.25e8, p = 64, K = 128           (1e9 rows / 1024 partitions on 8 GPUs)
 
@@ -40,6 +42,9 @@ FP64_MFMA_PEAK_TF = 78.6   # MI355X fp64 matrix (spec; = fp64 vector on CDNA4)
 CONFIGS = {
     2: dict(n=100_000_000, p=100, K=1024, family="logistic",
             name="config2: synthetic logistic n=1e8 rows/GPU, p=100, K=1024 partitions/GPU"),
+    3: dict(n=15_000_000, p=181, K=128, family="logistic", data="dummy", intercept=True,
+            name="config3: airline-like logistic n=1.5e7 rows/GPU (1.2e8 on 8 GPUs), 9 numeric + "
+                 "172 dummy columns + intercept, K=128 partitions/GPU"),
     5: dict(n=5_000_000, p=500, K=32, family="logistic",
             name="config5: synthetic logistic n=5e6 rows/GPU, p=500, K=32 partitions/GPU (wide path)"),
     4: dict(n=125_000_000, p=64, K=128, family="ols",
@@ -50,13 +55,23 @@ CONFIGS = {
 def _cpu_worker(args):
     """One partition of the CPU baseline: regenerate its rows from the counter
     stream, fit with the numpy oracle (1 BLAS thread)."""
-    n, p, seed, row0, family = args
+    n, p, seed, row0, family, data = args
+    import numpy as np
     from threadpoolctl import threadpool_limits
 
     import oracle as O
 
     with threadpool_limits(1):
-        X, y = O.simulate_counter(n, p, seed=seed, row0=row0)
+        if data == "dummy":
+            import torch
+
+            from dlsa_amd.models import simulate_dummy_design
+            torch.set_num_threads(1)
+            Xt, yt = simulate_dummy_design(n, seed=seed + row0, device="cpu")
+            X, y = Xt.numpy(), yt.numpy()
+            X = np.hstack([np.ones((n, 1)), X])  # intercept column
+        else:
+            X, y = O.simulate_counter(n, p, seed=seed, row0=row0)
         t0 = time.perf_counter()
         if family == "ols":
             O.ols_fit(X, y)
@@ -66,13 +81,13 @@ def _cpu_worker(args):
         return time.perf_counter() - t0, it
 
 
-def cpu_baseline(nk, p, n_parts, workers, family, seed=2019):
+def cpu_baseline(nk, p, n_parts, workers, family, seed=2019, data="counter"):
     """Oracle (port) timed on host cores: n_parts partitions of nk rows, one
     process per core, fit time only (data regeneration excluded)."""
     import multiprocessing as mp
 
     ctx = mp.get_context("spawn")
-    jobs = [(nk, p, seed, k * nk, family) for k in range(n_parts)]
+    jobs = [(nk, p, seed, k * nk, family, data) for k in range(n_parts)]
     t0 = time.perf_counter()
     with ctx.Pool(workers) as pool:
         res = pool.map(_cpu_worker, jobs, chunksize=1)
@@ -80,7 +95,7 @@ def cpu_baseline(nk, p, n_parts, workers, family, seed=2019):
     fit_s = sum(r[0] for r in res)
     rows_per_s = n_parts * nk / (fit_s / workers)  # all `workers` cores fitting concurrently
     return {"value": rows_per_s, "unit": "rows/s", "cores": workers, "kind": "port",
-            "sample": f"{n_parts} partitions x {nk} rows x p={p}, numpy fp64 "
+            "sample": f"{n_parts} partitions x {nk} rows x p={p}{' (dummy design + intercept)' if data == 'dummy' else ''}, numpy fp64 "
                       f"{'OLS' if family == 'ols' else 'IRLS'} oracle, 1 BLAS thread per process, "
                       f"{workers} processes; fit CPU time {fit_s:.1f} s, wall {wall:.1f} s incl. "
                       f"data regeneration",
@@ -120,15 +135,22 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from dlsa_amd import _hip
-    from dlsa_amd.dlsa import reduce_partitions_device, split_reduced
+    from dlsa_amd.dlsa import reduce_partitions_device, split_reduced, wlse
     from dlsa_amd.lsa import lars_lsa
-    from dlsa_amd.models import logistic_model_batched, ols_model_batched, simulate_logistic_device
+    from dlsa_amd.models import (logistic_model_batched, ols_model_batched, simulate_dummy_design,
+                                 simulate_logistic_device)
 
     n, p, K, family = cfg["n"], cfg["p"], cfg["K"], cfg["family"]
-    P = p
+    data = cfg.get("data", "counter")
+    fit_intercept = bool(cfg.get("intercept", False))
+    P = p + int(fit_intercept)
     wide = P > _hip.MAX_P_FUSED
     offsets = (np.arange(K + 1, dtype=np.int64) * n) // K
-    X, y = simulate_logistic_device(n, p, seed=args.seed, row0=rank * n, device=dev)
+    if data == "dummy":
+        X, y = simulate_dummy_design(n, seed=args.seed + rank, device=dev)
+        assert X.shape[1] == p
+    else:
+        X, y = simulate_logistic_device(n, p, seed=args.seed, row0=rank * n, device=dev)
     if family == "ols":  # linear response on the same design
         y = X[:, : max(1, int(0.4 * p))].sum(1) + 0.5 * (y - 0.5)
     ws = torch.empty((1,), dtype=torch.uint8, device=dev)
@@ -142,7 +164,8 @@ def main():
         if family == "ols":
             fit = ols_model_batched(X, y, offsets, record_timing=record, device=dev)
         else:
-            fit = logistic_model_batched(X, y, offsets, hessian=args.hessian, tol=args.tol,
+            fit = logistic_model_batched(X, y, offsets, fit_intercept=fit_intercept,
+                                         hessian=args.hessian, tol=args.tol,
                                          record_timing=record, workspace=ws, device=dev)
             if ws.numel() < fit.stats["workspace_bytes"]:
                 ws = torch.empty((fit.stats["workspace_bytes"],), dtype=torch.uint8, device=dev)
@@ -150,11 +173,11 @@ def main():
         if world > 1:
             dist.all_reduce(buf, op=dist.ReduceOp.SUM)  # RCCL over xGMI
         S, v, st, Ksum = split_reduced(buf.cpu().numpy(), fit.P)
-        wlse = np.linalg.lstsq(S, v, rcond=None)[0]
-        lars = lars_lsa(S, wlse, False, n_global, type="lasso")
+        est = wlse(S, v)
+        lars = lars_lsa(S, est, fit_intercept, n_global, type="lasso")
         ib = int(np.argmin(lars["BIC"]))
         support = np.nonzero(lars["beta"][ib])[0]
-        return fit, wlse, support
+        return fit, est, support
 
     for _ in range(args.warmup):
         step(False)
@@ -163,7 +186,7 @@ def main():
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        fit, wlse, support = step(True)
+        fit, est, support = step(True)
         stats_acc.append(fit.stats)
     torch.cuda.synchronize()
     if world > 1:
@@ -180,7 +203,7 @@ def main():
     # (HIP events recorded on the fit's stream around every launch)
     tot = lambda key: sum(s[key] for s in stats_acc)  # noqa: E731
     row_bytes = 8 * p + 8                        # X row + y, read once per pass
-    alg_flops_row = p * (p + 1) + 4 * p + 20     # symmetric X^T W X + X.b, X^T r
+    alg_flops_row = P * (P + 1) + 4 * P + 20     # symmetric X^T W X + X.b, X^T r
     kern = {}
     if wide:
         NB = (P + 127) // 128
@@ -266,10 +289,14 @@ def main():
         "metric": METRIC, "value": value, "unit": "rows/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-        "data": "synthetic: X~U(-1/2,1/2), beta*=1 on first floor(0.4p) cols, y~Bernoulli"
+        "data": ("synthetic airline-like: 9 U(-1/2,1/2) numeric + dummies of 5 skewed factors "
+                 "(12/7/20/69/69 levels, baseline dropped), y~Bernoulli(sigmoid(-0.3+X beta*)); "
+                 "torch generator in HBM (not timed)") if data == "dummy" else
+                "synthetic: X~U(-1/2,1/2), beta*=1 on first floor(0.4p) cols, y~Bernoulli"
                 "(sigmoid(X beta*)); counter-based generator in HBM (not timed)",
         "config": {"workload": cfg["name"] + " + DLSA combine + LARS/DBIC",
-                   "n_rows_per_gpu": n, "p": p, "partitions_per_gpu": K,
+                   "n_rows_per_gpu": n, "p": p, "P": P, "fit_intercept": fit_intercept,
+                   "partitions_per_gpu": K,
                    "family": family, "hessian": args.hessian if family == "logistic" else "fp64",
                    "tol": args.tol,
                    "parallelism": f"dp{world} (partitions sharded; 1 RCCL all-reduce of P^2+2P+1 fp64)"},
@@ -287,7 +314,7 @@ def main():
             nk_cpu, parts = 20000, 16      # ~8 s of single-thread work per partition
         else:
             nk_cpu, parts = n // K, args.cpu_parts
-        out["cpu_baseline"] = cpu_baseline(nk_cpu, p, parts, workers, family)
+        out["cpu_baseline"] = cpu_baseline(nk_cpu, p, parts, workers, family, data=data)
         out["vs_cpu_baseline"] = value / out["cpu_baseline"]["value"]
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -30,6 +30,27 @@ void set_error(const std::string& msg);
 
 namespace {
 
+// y += alpha x
+inline void axpy(
+    int n, double alpha, const double* __restrict x, double* __restrict y) {
+  for (int i = 0; i < n; ++i) y[i] += alpha * x[i];
+}
+
+// sum_i x[i] y[i] with 4 partial sums
+inline double dot(
+    int n, const double* __restrict x, const double* __restrict y) {
+  double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+  int i = 0;
+  for (; i + 4 <= n; i += 4) {
+    s0 += x[i] * y[i];
+    s1 += x[i + 1] * y[i + 1];
+    s2 += x[i + 2] * y[i + 2];
+    s3 += x[i + 3] * y[i + 3];
+  }
+  for (; i < n; ++i) s0 += x[i] * y[i];
+  return (s0 + s1) + (s2 + s3);
+}
+
 struct Chol {
   // upper-triangular R (d x d) stored with leading dimension m
   int m = 0, d = 0;
@@ -38,19 +59,21 @@ struct Chol {
   double& at(int i, int j) { return r[(size_t)i * m + j]; }
   double at(int i, int j) const { return r[(size_t)i * m + j]; }
   // solve R^T x = b (forward)
+  // (column-oriented: row k of R is contiguous; x[i] still subtracts its
+  // terms in k order, so the rounding is that of the dot-product form)
   void solve_rt(const double* b, double* x) const {
-    for (int i = 0; i < d; ++i) {
-      double s = b[i];
-      for (int k = 0; k < i; ++k) s -= at(k, i) * x[k];
-      x[i] = s / at(i, i);
+    for (int i = 0; i < d; ++i) x[i] = b[i];
+    for (int k = 0; k < d; ++k) {
+      const double xk = x[k] / at(k, k);
+      x[k] = xk;
+      axpy(d - k - 1, -xk, &r[(size_t)k * m + k + 1], x + k + 1);
     }
   }
   // solve R x = b (backward)
   void solve_r(const double* b, double* x) const {
     for (int i = d - 1; i >= 0; --i) {
-      double s = b[i];
-      for (int k = i + 1; k < d; ++k) s -= at(i, k) * x[k];
-      x[i] = s / at(i, i);
+      const double* ri = &r[(size_t)i * m];
+      x[i] = (b[i] - dot(d - i - 1, ri + i + 1, x + i + 1)) / ri[i];
     }
   }
 };
@@ -178,13 +201,18 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
     w.assign(na, 0.0);
     for (int q = 0; q < na; ++q) w[q] = A * Gi1[q];
     double gamhat = Cmax / A;
+    // a = Sigma[:, active] w, accumulated over q in order as contiguous row
+    // axpys (Sigma is symmetric): the equiangular correlations of every
+    // column, used by the step length and by the correlation update
+    a.assign(m, 0.0);
+    for (int q = 0; q < na; ++q)
+      axpy(m, w[q], &Sig[(size_t)active[q] * m], a.data());
     if (na < m) {
       keep.clear();
       for (int j = 0; j < m; ++j)
         if (!in_active[j] && !in_ignores[j]) keep.push_back(j);
       for (int j : keep) {
-        double aj = 0;
-        for (int q = 0; q < na; ++q) aj += w[q] * S(active[q], j);
+        const double aj = a[j];
         const double c = Cvec[j];
         const double g1 = (Cmax - c) / (A - aj), g2 = (Cmax + c) / (A + aj);
         if (g1 > eps) gamhat = std::min(gamhat, g1);
@@ -208,11 +236,7 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
     }
     for (int j = 0; j < m; ++j) B(k, j) = B(k - 1, j);
     for (int q = 0; q < na; ++q) B(k, active[q]) += gamhat * w[q];
-    for (int j = 0; j < m; ++j) {
-      double s = 0;
-      for (int q = 0; q < na; ++q) s += S(j, active[q]) * w[q];
-      Cvec[j] -= gamhat * s;
-    }
+    for (int j = 0; j < m; ++j) Cvec[j] -= gamhat * a[j];
     if (lasso && any_drop) {
       for (int q = na - 1; q >= 0; --q) {
         if (!drops[q]) continue;
@@ -269,12 +293,12 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
   std::vector<double> dff(m), tmp(m);
   for (int s = 0; s < nst; ++s) {
     for (int j = 0; j < m; ++j) dff[j] = sgnb[j] - B(s, j);
+    // rss = dff^T Sigma dff: e = Sigma dff as row axpys (Sigma symmetric,
+    // contiguous rows vectorise), then dff . e
+    std::fill(tmp.begin(), tmp.end(), 0.0);
+    for (int j = 0; j < m; ++j) axpy(m, dff[j], &Sig[(size_t)j * m], tmp.data());
     double rss = 0;
-    for (int i = 0; i < m; ++i) {
-      double t = 0;
-      for (int j = 0; j < m; ++j) t += S(i, j) * dff[j];
-      rss += dff[i] * t;
-    }
+    for (int i = 0; i < m; ++i) rss += dff[i] * tmp[i];
     int dof = 0;
     double b0s = beta0_init;
     for (int j = 0; j < m; ++j) {

@@ -35,6 +35,15 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+typedef double d4s __attribute__((ext_vector_type(4)));
+
+// v_readlane of a double (lane index wave-uniform)
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
+
 // Packed lower triangle: element (i, j), i >= j, at i (i + 1) / 2 + j.
 __device__ __forceinline__ int tri(int i, int j) { return i * (i + 1) / 2 + j; }
 
@@ -52,13 +61,16 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
   double* H = sm;                    // packed lower triangle, P (P + 1) / 2
   double* g = H + P * (P + 1) / 2;   // PP
   double* z = g + PP;                // PP
-  double* red = z + PP;              // 8: [0..3] block reductions, [6] flag, [7] ll
+  double* invd = z + PP;             // PP: 1 / L_jj
+  double* red = invd + PP;           // 8: [0..3] block reductions, [5] flag, [7] ll
 
-  const int cb = a.part_chunk_begin[k], ce = a.part_chunk_begin[k + 1];
+  // chunk partials were summed into the partition's first chunk by
+  // partials_sum_kernel (fixed chunk order)
+  const int cb = a.part_chunk_begin[k], ce = min(a.part_chunk_begin[k + 1], cb + 1);
   const int phase = a.phase[k];
 
   // 1. assemble: thread tid owns element (tile t, position tid) of every
-  //    tile; the chunk loop issues T independent loads per step.  Only the
+  //    tile.  Only the
   //    lower triangle is kept (diagonal tiles hold (w x_i) x_j and (w x_j) x_i,
   //    equal up to the last bit): Sig_inv comes out exactly symmetric.
   {
@@ -143,41 +155,104 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
   }
   __syncthreads();
 
-  // 4. Cholesky, right-looking, lower, in place.  Thread (tid/2, tid%2) owns
-  //    the even/odd columns of rows tid/2, tid/2 + 128.  Column j is only READ
-  //    during step j (l_xj = H[x][j] / sqrt(H[j][j]) recomputed by every
-  //    reader); its scaled values are written back at step j+1, so one
-  //    barrier per column suffices.
-  const int row0 = tid >> 1, par = tid & 1;
+  // 4. Cholesky, blocked (16-column panels), lower, in place in the packed
+  //    triangle.  Per panel b (columns c0 .. c0 + 15):
+  //    (a) wave 0 factors the diagonal block in registers (lane i = row i,
+  //        column values broadcast with v_readlane) and records 1 / L_jj;
+  //    (b) every thread solves one row i of the panel below:
+  //        L_ib = A_ib L_bb^-T (forward substitution against L_bb);
+  //    (c) the trailing lower triangle is updated tile by tile on fp64 MFMA,
+  //        A_IJ -= L_Ib L_Jb^T (16x16 tiles, 4 k-steps of 4 columns).
+  //    Three barriers per 16 columns (was one per column with a serial
+  //    per-thread row update).
+  if (tid == 0) red[5] = 0.0;
+  __syncthreads();
   bool ok = true;
-  double inv_prev = 0.0;
-  for (int j = 0; j < P; ++j) {
-    const double d = H[tri(j, j)];
-    if (!(d > 0.0) || !isfinite(d)) {
-      ok = false;  // uniform: every thread read the same d
+  for (int b = 0; b < NT; ++b) {
+    const int c0 = 16 * b;
+    if (c0 >= P) break;
+    const int nb = min(16, P - c0);
+    if (wid == 0) {
+      const int i = lane & 15;
+      const bool act = lane < nb;
+      double av[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) av[j] = (act && j <= i) ? H[tri(c0 + i, c0 + j)] : 0.0;
+      bool good = true;
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) {
+        if (kk < nb) {  // wave-uniform
+          const double dkk = readlane_f64(av[kk], kk);
+          good = good && dkk > 0.0 && isfinite(dkk);
+          const double lkk = sqrt(dkk);
+          const double il = 1.0 / lkk;
+          av[kk] = (i > kk) ? av[kk] * il : (i == kk ? lkk : av[kk]);
+#pragma unroll
+          for (int j = kk + 1; j < 16; ++j) {
+            const double ljk = readlane_f64(av[kk], j);  // L[j][kk], row j's lane
+            if (j <= i) av[j] = fma(-av[kk], ljk, av[j]);
+          }
+          if (lane == 0) invd[c0 + kk] = il;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (act && j <= i) H[tri(c0 + i, c0 + j)] = av[j];
+      if (lane == 0 && !good) red[5] = 1.0;
+    }
+    __syncthreads();
+    if (red[5] != 0.0) {  // block-uniform
+      ok = false;
       break;
     }
-    const double inv = 1.0 / sqrt(d);
-    const double* colj = H + j;  // H[tri(c, j)] = colj[c (c + 1) / 2]
-    for (int row = row0; row < P; row += 128) {
-      double* hr = H + tri(row, 0);
-      if (par == 0 && j > 0 && row >= j - 1) {
-        // deferred write-back of column j-1 (scaled) for this row
-        hr[j - 1] = (row == j - 1) ? sqrt(hr[row]) : hr[j - 1] * inv_prev;
+    if (c0 + 16 < P) {
+      const int i = c0 + 16 + tid;
+      if (i < P) {
+        double* hr = H + tri(i, c0);
+        double x[16];
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) x[kk] = hr[kk];
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) {
+          x[kk] *= invd[c0 + kk];
+#pragma unroll
+          for (int m = kk + 1; m < 16; ++m) x[m] = fma(-x[kk], H[tri(c0 + m, c0 + kk)], x[m]);
+        }
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) hr[kk] = x[kk];
       }
-      if (row > j) {
-        const double lij = hr[j] * inv;
-        for (int c = j + 1 + par; c <= row; c += 2) hr[c] -= lij * (colj[tri(c, 0)] * inv);
+      __syncthreads();
+      const int m = NT - b - 1;  // tile rows below the panel
+      const int ntile = m * (m + 1) / 2;
+      const int fl = lane & 15, q = lane >> 4;
+      for (int t = wid; t < ntile; t += 4) {  // wave-uniform
+        int I = 0;
+        while ((I + 1) * (I + 2) / 2 <= t) ++I;
+        const int J = t - I * (I + 1) / 2;
+        const int gI = c0 + 16 * (I + 1), gJ = c0 + 16 * (J + 1);
+        d4s acc;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = gI + q + 4 * r, col = gJ + fl;
+          acc[r] = (row < P && col <= row) ? H[tri(row, col)] : 0.0;
+        }
+        const int ra = gI + fl, rb = gJ + fl;
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+          const int kc = c0 + 4 * st + q;
+          const double x_a = ra < P ? H[tri(ra, kc)] : 0.0;
+          const double x_b = rb < P ? H[tri(rb, kc)] : 0.0;
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-x_a, x_b, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = gI + q + 4 * r, col = gJ + fl;
+          if (row < P && col <= row) H[tri(row, col)] = acc[r];
+        }
       }
     }
-    inv_prev = inv;
     __syncthreads();
   }
-  if (ok && par == 0 && row0 == (P - 1) % 128 && row0 < P) {
-    // last column: only the diagonal element
-    H[tri(P - 1, P - 1)] = sqrt(H[tri(P - 1, P - 1)]);
-  }
-  __syncthreads();
   if (!ok) {
     if (a.subsample) {
       level_fail();
@@ -207,7 +282,7 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
 #pragma unroll
       for (int r = 0; r < R; ++r)
         if ((j >> 6) == r) piv = zr[r];
-      const double zj = __shfl(piv, j & 63) / H[tri(j, j)];
+      const double zj = __shfl(piv, j & 63) * invd[j];
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const int i = lane + 64 * r;
@@ -222,7 +297,7 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
 #pragma unroll
       for (int r = 0; r < R; ++r)
         if ((j >> 6) == r) piv = zr[r];
-      const double zj = __shfl(piv, j & 63) / H[tri(j, j)];
+      const double zj = __shfl(piv, j & 63) * invd[j];
       const double* lj = H + tri(j, 0);
 #pragma unroll
       for (int r = 0; r < R; ++r) {
@@ -309,6 +384,53 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
   }
 }
 
+
+// Sum the per-chunk partials (Hessian tiles, gradient, log-likelihood) of
+// every running partition into its first chunk's slab, in chunk order
+// (deterministic).  Grid (ceil((T + 1) / 4), K): wave w of workgroup x owns
+// tile 4x + w (tile T = the gradient and log-likelihood), so a partition's
+// partials are read by many waves at once instead of by its single solve
+// workgroup (config 3: 65 chunks x 78 tiles per partition).
+__global__ __launch_bounds__(256) void partials_sum_kernel(const SolveArgs a, int T, int PP) {
+  const int k = blockIdx.y;
+  if (a.status[k] != STATUS_RUNNING) return;
+  const int cb = a.part_chunk_begin[k], n = a.part_chunk_begin[k + 1] - cb;
+  if (n <= 1) return;
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t < T) {
+    const int64_t stride = (int64_t)T * 256;
+    double* dst = const_cast<double*>(a.slab_H) + cb * stride + t * 256 + lane;
+    const double* src = dst;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+#pragma unroll 8
+    for (int c = 0; c < n; ++c) {
+      const double* p = src + c * stride;
+      s0 += p[0];
+      s1 += p[64];
+      s2 += p[128];
+      s3 += p[192];
+    }
+    dst[0] = s0;
+    dst[64] = s1;
+    dst[128] = s2;
+    dst[192] = s3;
+  } else if (t == T) {
+    double* g = const_cast<double*>(a.slab_g) + (int64_t)cb * PP;
+    for (int e = lane; e < PP; e += 64) {
+      double s = 0.0;
+#pragma unroll 8
+      for (int c = 0; c < n; ++c) s += g[(int64_t)c * PP + e];
+      g[e] = s;
+    }
+    double* ll = const_cast<double*>(a.slab_ll) + cb;
+    double s = 0.0;
+    for (int c = lane; c < n; c += 64) s += ll[c];
+    s = wave_sum(s);
+    if (lane == 0) ll[0] = s;
+  }
+}
+
 template <int NT>
 static hipError_t launch_solve_t(const SolveArgs& a, int K, size_t lds, hipStream_t s) {
   static bool attr_set = false;
@@ -318,13 +440,15 @@ static hipError_t launch_solve_t(const SolveArgs& a, int K, size_t lds, hipStrea
     if (e != hipSuccess) return e;
     attr_set = true;
   }
+  constexpr int T = NT * (NT + 1) / 2;
+  hipLaunchKernelGGL(partials_sum_kernel, dim3((T + 1 + 3) / 4, K), dim3(256), 0, s, a, T, 16 * NT);
   hipLaunchKernelGGL(newton_solve_kernel<NT>, dim3(K), dim3(256), lds, s, a);
   return hipGetLastError();
 }
 
 hipError_t launch_newton_solve(const SolveArgs& a, int K, hipStream_t s) {
   const int PP = 16 * a.NT;
-  const size_t lds = ((size_t)a.P * (a.P + 1) / 2 + 2 * PP + 8) * sizeof(double);
+  const size_t lds = ((size_t)a.P * (a.P + 1) / 2 + 3 * PP + 8) * sizeof(double);
   switch (a.NT) {
     case 1: return launch_solve_t<1>(a, K, lds, s);
     case 2: return launch_solve_t<2>(a, K, lds, s);

@@ -17,11 +17,34 @@ import numpy as np
 from . import _hip
 
 
+def wlse(S, v):
+    """WLSE = (sum Sig_inv)^-1 (sum Sig_inv theta) (dlsa.py:48-49).
+
+    The reference calls ``np.linalg.lstsq`` (an SVD).  ``sum Sig_inv`` is a sum
+    of positive-definite information matrices, so a Cholesky solve gives the
+    same solution (to rounding) at a fraction of the host time (P = 182: 0.3 ms
+    instead of 6 ms); a matrix that is not numerically positive definite
+    (e.g. an all-zero dummy column) falls back to the reference's lstsq,
+    whose minimum-norm solution is then the defined result."""
+    import scipy.linalg as sla
+
+    S = np.asarray(S, dtype=np.float64)
+    v = np.asarray(v, dtype=np.float64)
+    try:
+        c = sla.cho_factor(S, lower=True, check_finite=True)
+        x = sla.cho_solve(c, v, check_finite=False)
+        if np.all(np.isfinite(x)):
+            return x
+    except (np.linalg.LinAlgError, ValueError):
+        pass
+    return np.linalg.lstsq(S, v, rcond=None)[0]
+
+
 def _frame(S, v, sum_theta, K, columns):
     import pandas as pd
 
     p = v.size
-    beta_ols = np.linalg.lstsq(S, v, rcond=None)[0]          # dlsa.py:48-49
+    beta_ols = wlse(S, v)                                      # dlsa.py:48-49
     beta_oneshot = sum_theta / K                               # dlsa.py:51-52
     if columns is None:
         columns = [f"x{j}" for j in range(p)]

@@ -106,6 +106,48 @@ def simulate_logistic_device(n, p, seed=2019, row0=0, device=None):
     return X, y
 
 
+#: airline-like design of BASELINE config 3: numeric columns + dummy-coded
+#: factors (levels per factor; the first level of each is the dropped baseline,
+#: models.py:65-69 with ``dummy_factors_baseline``) -> 9 + 11 + 6 + 19 + 68 + 68
+#: = 181 columns, 182 parameters with the intercept.
+AIRLINE_NUMERIC = 9
+AIRLINE_FACTORS = (12, 7, 20, 69, 69)  # Month, DayOfWeek, UniqueCarrier, Origin, Dest
+
+
+def simulate_dummy_design(n, seed=2019, numeric=AIRLINE_NUMERIC, factors=AIRLINE_FACTORS,
+                          device=None):
+    """Synthetic airline-like logistic data (BASELINE config 3), generated with
+    torch ops on ``device`` ("cpu" allowed: test and baseline plumbing).
+
+    Columns: ``numeric`` U(-1/2, 1/2) features, then for each factor with L
+    levels the L-1 dummy columns of levels 1..L-1 (level 0 is the baseline);
+    codes are skewed towards low levels (code = floor(L u^2)) like airport and
+    carrier frequencies.  y ~ Bernoulli(sigmoid(-0.3 + X beta*)) with
+    beta*_numeric ~ U(-1, 1) and dummy effects ~ 0.3 N(0, 1) (fixed by
+    ``seed``; the rows by ``seed`` too).  Returns (X [n, p] fp64, y [n] fp64);
+    fit it with ``fit_intercept=True``."""
+    dev = torch.device(device) if device is not None else torch.device("cuda")
+    n = int(n)
+    p = numeric + sum(L - 1 for L in factors)
+    gb = torch.Generator(device="cpu").manual_seed(int(seed) ^ 0x5EED)
+    beta = torch.cat([torch.rand(numeric, generator=gb, dtype=torch.float64) * 2 - 1,
+                      0.3 * torch.randn(p - numeric, generator=gb, dtype=torch.float64)])
+    g = torch.Generator(device=dev).manual_seed(int(seed))
+    X = torch.zeros((n, p), dtype=torch.float64, device=dev)
+    X[:, :numeric] = torch.rand((n, numeric), generator=g, dtype=torch.float64, device=dev) - 0.5
+    rows = torch.arange(n, device=dev)
+    col = numeric
+    for L in factors:
+        u = torch.rand((n,), generator=g, dtype=torch.float64, device=dev)
+        code = torch.clamp((L * u * u).long(), max=L - 1)
+        m = code > 0
+        X[rows[m], col + code[m] - 1] = 1.0
+        col += L - 1
+    eta = X @ beta.to(dev) - 0.3
+    y = (torch.rand((n,), generator=g, dtype=torch.float64, device=dev) < torch.sigmoid(eta)).double()
+    return X, y
+
+
 def partition_offsets(partition_id, num_partitions=None):
     """Group rows by partition id: returns (order, offsets) so that rows
     ``order[offsets[k]:offsets[k+1]]`` are partition k in their original order

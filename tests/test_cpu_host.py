@@ -197,3 +197,43 @@ def test_distributed_combine_gloo(golden_dir):
         assert np.abs(wlse - g["wlse_noint"]).max() < 1e-10
         assert np.abs(oneshot - g["oneshot_noint"]).max() < 1e-12
         assert support == [0, 1, 2, 3]
+
+
+def test_dummy_design_generator():
+    """Config-3 generator: 181 columns, at most one dummy set per factor per
+    row, deterministic in the seed, every level present at moderate n."""
+    torch = pytest.importorskip("torch")
+    from dlsa_amd.models import AIRLINE_FACTORS, AIRLINE_NUMERIC, simulate_dummy_design
+
+    X, y = simulate_dummy_design(30000, seed=3, device="cpu")
+    X2, y2 = simulate_dummy_design(30000, seed=3, device="cpu")
+    assert X.shape == (30000, 181) and torch.equal(X, X2) and torch.equal(y, y2)
+    num = X[:, :AIRLINE_NUMERIC]
+    assert float(num.min()) >= -0.5 and float(num.max()) < 0.5
+    col = AIRLINE_NUMERIC
+    for L in AIRLINE_FACTORS:
+        block = X[:, col:col + L - 1]
+        assert set(block.unique().tolist()) <= {0.0, 1.0}
+        assert float(block.sum(1).max()) <= 1.0
+        assert bool((block.sum(0) > 0).all())
+        col += L - 1
+    assert set(y.unique().tolist()) == {0.0, 1.0}
+
+
+def test_wlse_cholesky_matches_lstsq_and_falls_back():
+    """dlsa.py:48-49 solves with lstsq; the Cholesky solve agrees on a positive-
+    definite sum and a singular sum (an all-zero dummy column) keeps lstsq's
+    minimum-norm answer."""
+    from dlsa_amd.dlsa import wlse
+
+    rng = np.random.default_rng(5)
+    A = rng.standard_normal((400, 60))
+    S = A.T @ A
+    v = rng.standard_normal(60)
+    ref = np.linalg.lstsq(S, v, rcond=None)[0]
+    assert np.abs(wlse(S, v) - ref).max() < 1e-12 * np.abs(ref).max()
+    S[7, :] = 0.0
+    S[:, 7] = 0.0
+    v[7] = 0.0
+    ref = np.linalg.lstsq(S, v, rcond=None)[0]
+    assert np.allclose(wlse(S, v), ref, rtol=1e-10, atol=1e-12)

@@ -236,6 +236,25 @@ def test_config2_shape_sampled_partitions(torch_cuda, M):
         assert gk.abs().max().item() < 1e-6
 
 
+def test_config3_dummy_design_vs_oracle(torch_cuda, M):
+    """BASELINE config-3 geometry: airline-like design (9 numeric + 172 dummy
+    columns, intercept -> P = 182, the 8-wave NT = 12 pass) generated on the
+    device; every partition (ragged sizes) against the oracle, mixed
+    Hessian."""
+    torch = torch_cuda
+    X, y = M.simulate_dummy_design(4 * 20000 + 7, seed=7, device="cuda")
+    off = np.array([0, 20000, 40003, 60001, 80007], dtype=np.int64)
+    fit = M.logistic_model_batched(X, y, off, fit_intercept=True)
+    Xh, yh = X.cpu().numpy(), y.cpu().numpy()
+    th, S, St, ll, it = O.logistic_fit_partitions(Xh, yh, off, fit_intercept=True)
+    assert (fit.status.cpu().numpy() == 0).all()
+    assert fit.theta.shape == (4, 182)
+    assert _rel(fit.theta.cpu(), th) < REL
+    assert _rel(fit.sig_inv.cpu(), S) < REL
+    assert _rel(fit.sig_inv_theta.cpu(), St) < REL
+    assert _rel(fit.loglik.cpu(), ll) < 1e-10
+
+
 @pytest.mark.parametrize("p,fi", [(8, True), (64, False), (100, True)])
 def test_ols_vs_oracle(torch_cuda, M, p, fi):
     """Linear DLSA path (config 4 shape at small n): closed-form OLS per
