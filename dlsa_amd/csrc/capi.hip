@@ -298,32 +298,54 @@ int dlsa_last_fit_stats(dlsa_fit_stats* out) {
 
 namespace dlsa {
 
-// Event timer of the fit's stream (record_timing only).
+// Event timer of the fit's stream (record_timing only).  A pair of events
+// brackets every launch; the elapsed times are read after the fit's final
+// stream synchronisation (flush), so timing adds no host round trip per
+// launch and the launches stay queued back to back.
 struct StreamTimer {
   hipStream_t stream;
   bool on;
-  hipEvent_t ev[2] = {nullptr, nullptr};
-  hipError_t init() {
-    if (!on) return hipSuccess;
-    hipError_t e = hipEventCreate(&ev[0]);
-    if (e == hipSuccess) e = hipEventCreate(&ev[1]);
-    return e;
-  }
+  std::vector<hipEvent_t> ev;        // 2 per recorded launch, reused across calls
+  std::vector<double*> dst_a, dst_b; // accumulators of each recorded launch
+  size_t used = 0;
+  hipError_t init() { return hipSuccess; }
   ~StreamTimer() {
-    if (ev[0]) (void)hipEventDestroy(ev[0]);
-    if (ev[1]) (void)hipEventDestroy(ev[1]);
+    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
   }
   template <typename F>
-  hipError_t operator()(double* acc, F&& launch) {
+  hipError_t operator()(double* acc, F&& launch, double* acc2 = nullptr) {
     if (!on) return launch();
-    hipError_t e = hipEventRecord(ev[0], stream);
+    if (2 * used + 2 > ev.size()) {
+      for (int i = 0; i < 2; ++i) {
+        hipEvent_t e = nullptr;
+        hipError_t r = hipEventCreate(&e);
+        if (r != hipSuccess) return r;
+        ev.push_back(e);
+      }
+    }
+    hipError_t e = hipEventRecord(ev[2 * used], stream);
     if (e == hipSuccess) e = launch();
-    if (e == hipSuccess) e = hipEventRecord(ev[1], stream);
-    if (e == hipSuccess) e = hipEventSynchronize(ev[1]);
-    float ms = 0.f;
-    if (e == hipSuccess) e = hipEventElapsedTime(&ms, ev[0], ev[1]);
-    *acc += ms;
-    return e;
+    if (e == hipSuccess) e = hipEventRecord(ev[2 * used + 1], stream);
+    if (e != hipSuccess) return e;
+    dst_a.push_back(acc);
+    dst_b.push_back(acc2);
+    ++used;
+    return hipSuccess;
+  }
+  // after the stream has been synchronised
+  hipError_t flush() {
+    for (size_t i = 0; i < used; ++i) {
+      float ms = 0.f;
+      hipError_t e = hipEventSynchronize(ev[2 * i + 1]);
+      if (e == hipSuccess) e = hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]);
+      if (e != hipSuccess) return e;
+      *dst_a[i] += ms;
+      if (dst_b[i]) *dst_b[i] += ms;
+    }
+    used = 0;
+    dst_a.clear();
+    dst_b.clear();
+    return hipSuccess;
   }
 };
 
@@ -491,27 +513,22 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
     sa.switch_tol = final_level ? opt.switch_tol : 0.0;
     const int it_end = final_level ? max_iter : std::min(max_iter, it + 10);
     for (; it < it_end && (n_running[0] + n_running[1]) > 0 && q.rows.n_chunks > 0; ++it) {
-      double ms_row = 0.0;
-      DLSA_HIP_TRY(timed(&ms_row, [&] {
+      DLSA_HIP_TRY(timed(&g_stats.ms_wide_row, [&] {
         return launch_wide_row(wa, standardize, family, q.rows.n_chunks, stream);
       }));
-      g_stats.ms_wide_row += ms_row;
       for (int ph = 0; ph < 2; ++ph) {
         if (n_running[ph] == 0) continue;
         wa.want_phase = ph;
-        double ms_gram = 0.0;
-        DLSA_HIP_TRY(timed(&ms_gram, [&] {
-          return launch_wide_gram(wa, standardize, ph == PHASE_F64, stream);
-        }));
-        g_stats.ms_wide_gram += ms_gram;
+        DLSA_HIP_TRY(timed(
+            &g_stats.ms_wide_gram,
+            [&] { return launch_wide_gram(wa, standardize, ph == PHASE_F64, stream); },
+            ph == PHASE_F64 ? &g_stats.ms_pass_fp64 : &g_stats.ms_pass_fp32));
         if (ph == PHASE_F64) {
           g_stats.passes_fp64++;
           g_stats.rows_fp64 += rows;
-          g_stats.ms_pass_fp64 += ms_gram;
         } else {
           g_stats.passes_fp32++;
           g_stats.rows_fp32 += rows;
-          g_stats.ms_pass_fp32 += ms_gram;
         }
       }
       DLSA_HIP_TRY(timed(&g_stats.ms_wide_assemble,
@@ -531,6 +548,7 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
   g_stats.ms_total =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start)
           .count();
+  DLSA_HIP_TRY(timed.flush());
   return DLSA_OK;
 }
 
@@ -723,33 +741,7 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
   sa.switch_tol = opt.switch_tol;
 
   const bool standardize = center != nullptr;
-  hipEvent_t ev[2] = {nullptr, nullptr};
-  if (opt.record_timing) {
-    DLSA_HIP_TRY(hipEventCreate(&ev[0]));
-    DLSA_HIP_TRY(hipEventCreate(&ev[1]));
-  }
-  struct EvFree {
-    hipEvent_t* e;
-    ~EvFree() {
-      if (e[0]) (void)hipEventDestroy(e[0]);
-      if (e[1]) (void)hipEventDestroy(e[1]);
-    }
-  } evfree{ev};
-  auto timed = [&](double* acc, auto&& launch) -> hipError_t {
-    if (!opt.record_timing) return launch();
-    hipError_t e = hipEventRecord(ev[0], stream);
-    if (e != hipSuccess) return e;
-    e = launch();
-    if (e != hipSuccess) return e;
-    e = hipEventRecord(ev[1], stream);
-    if (e != hipSuccess) return e;
-    e = hipEventSynchronize(ev[1]);
-    if (e != hipSuccess) return e;
-    float ms = 0.f;
-    e = hipEventElapsedTime(&ms, ev[0], ev[1]);
-    *acc += ms;
-    return e;
-  };
+  StreamTimer timed{stream, opt.record_timing != 0};
 
   int32_t* h_cnt = nullptr;
   DLSA_HIP_TRY(hipHostMalloc((void**)&h_cnt, 16, hipHostMallocDefault));
@@ -861,6 +853,7 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
   g_stats.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() -
                                                                t_start)
                          .count();
+  DLSA_HIP_TRY(timed.flush());
   return DLSA_OK;
 }
 
