@@ -77,22 +77,33 @@ __device__ __forceinline__ double dpp_f64(double v) {
   const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
   return __hiloint2double(hi, lo);
 }
-// Sum over the LPR (8 or 16) lanes of a row group.  8: quad xor1, quad xor2,
-// half-row mirror; 16: row_ror 8, 4, 2, 1.  Every lane ends with the
+// Lane l and lane l ^ 16 (permlane16_swap), l and l ^ 32 (permlane32_swap):
+// both operands are v, so the swapped pair (x, y) holds the two halves and
+// x + y is the same sum, bitwise, in both lanes of the pair.
+__device__ __forceinline__ double xor16_sum(double v) {
+  const unsigned lo = __double2loint(v), hi = __double2hiint(v);
+  const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  return __hiloint2double(b[0], a[0]) + __hiloint2double(b[1], a[1]);
+}
+__device__ __forceinline__ double xor32_sum(double v) {
+  const unsigned lo = __double2loint(v), hi = __double2hiint(v);
+  const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  return __hiloint2double(b[0], a[0]) + __hiloint2double(b[1], a[1]);
+}
+
+// Sum over the lanes l, l ^ RPW, l ^ 2 RPW, ... (the LPR feature groups of one
+// row in the row phase) without LDS: row_ror 8 (and 4) inside a 16-lane DPP
+// row, then the cross-row swaps.  Every lane of the row ends with the
 // bitwise-identical total (each step adds a commutative pair).
-template <int LPR>
+template <int RPW>
 __device__ __forceinline__ double red_row(double v) {
-  if constexpr (LPR == 8) {
-    v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
-    v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
-    v += dpp_f64<0x141>(v);  // row_half_mirror
-  } else {
-    static_assert(LPR == 16, "8 or 16 lanes per row");
-    v += dpp_f64<0x128>(v);
-    v += dpp_f64<0x124>(v);
-    v += dpp_f64<0x122>(v);
-    v += dpp_f64<0x121>(v);
-  }
+  static_assert(RPW == 8 || RPW == 4, "4 or 8 rows per wave");
+  v += dpp_f64<0x128>(v);                         // row_ror 8: l ^ 8
+  if constexpr (RPW == 4) v += dpp_f64<0x124>(v);  // row_ror 4: l + 4, l + 12
+  v = xor16_sum(v);
+  v = xor32_sum(v);
   return v;
 }
 
@@ -368,17 +379,19 @@ void irls_coop_kernel(const PassArgs a) {
       const bool valid = rB < rows_left;
       const double* xr = xs + rB * p + (sl - ic);
       double xv[M];
-      double e = 0.0;
+      double e0 = 0.0, e1 = 0.0;  // two FMA chains: half the latency of the dot product
 #pragma unroll
       for (int m = 0; m < M; ++m) {
         double v = xr[LPR * m];
         if constexpr (STD) v = (v - stdv[sl + LPR * m]) * stdv[G::PMAX + sl + LPR * m];
         if (m == 0 && ic && sl == 0) v = 1.0;
         xv[m] = v;
-        e = fma(v, beta[m], e);
+        if (m & 1)
+          e1 = fma(v, beta[m], e1);
+        else
+          e0 = fma(v, beta[m], e0);
       }
-#pragma unroll
-      for (int o = RPW; o < 64; o <<= 1) e += __shfl_xor(e, o);  // bitwise-identical in all lanes
+      const double e = red_row<RPW>(e0 + e1);  // bitwise-identical in all lanes of the row
       const double yv = ys[rB];
       double w, r;
       if constexpr (FAM == FAMILY_LOGISTIC && DLSA_ABLATE == 2) {
