@@ -79,6 +79,9 @@ def main():
     for r in range(args.rounds):
         for name, lib in libs.items():
             for kn in knobs:
+                for other in knobs:  # knobs of the other settings do not leak
+                    for kv in [x for x in other.split(",") if x]:
+                        os.environ.pop(kv.split("=")[0], None)
                 for kv in [x for x in kn.split(",") if x]:
                     k, v = kv.split("=")
                     os.environ[k] = v
