@@ -97,12 +97,24 @@ static int auto_rows_per_chunk(int64_t n_total, int NT = 0) {
 
 // rows_used(k) = clamp(ceil(frac * n_k), min_rows, n_k): a prefix of each
 // partition (frac = 1: all rows).
+static int64_t rows_used(int64_t nk, double frac, int64_t min_rows) {
+  if (frac >= 1.0) return nk;
+  return std::min(nk, std::max(min_rows, (int64_t)std::ceil(frac * (double)nk)));
+}
+static int64_t level_rows(const int64_t* offsets, int K, double frac, int64_t min_rows) {
+  int64_t n = 0;
+  for (int k = 0; k < K; ++k) n += std::max<int64_t>(0, rows_used(offsets[k + 1] - offsets[k], frac, min_rows));
+  return n;
+}
+
 static bool make_plan(const int64_t* offsets, int K, int p, int intercept, int rows_per_chunk,
                       Plan& pl, double frac = 1.0, int64_t min_rows = 0) {
   pl.P = p + (intercept ? 1 : 0);
   pl.NT = (pl.P + 15) / 16;
   pl.T = pl.NT * (pl.NT + 1) / 2;
   pl.PP = 16 * pl.NT;
+  // fused pass: chunk size from all rows (a warm-start level keeps the full
+  // pass's chunk size: fewer, equally long chunks -- measured as fast)
   const int64_t n_total = offsets[K];
   const int rpc = rows_per_chunk > 0 ? rows_per_chunk : auto_rows_per_chunk(n_total, pl.NT);
   pl.part_chunk_begin.assign(K + 1, 0);
@@ -113,8 +125,7 @@ static bool make_plan(const int64_t* offsets, int K, int p, int intercept, int r
     pl.part_chunk_begin[k] = (int32_t)pl.chunk_row0.size();
     const int64_t a = offsets[k];
     const int64_t nk = offsets[k + 1] - a;
-    int64_t n = nk;
-    if (frac < 1.0) n = std::min(nk, std::max(min_rows, (int64_t)std::ceil(frac * (double)nk)));
+    const int64_t n = rows_used(nk, frac, min_rows);
     if (n <= 0) continue;
     const int64_t nc = (n + rpc - 1) / rpc;
     for (int64_t c = 0; c < nc; ++c) {
@@ -173,7 +184,9 @@ struct WidePlans {
 static void make_wide_plans(const int64_t* offsets, int K, int p, int intercept,
                             int rows_per_chunk, WidePlans& wp, double frac = 1.0,
                             int64_t min_rows = 0) {
-  const int64_t n_total = offsets[K];
+  // wide path: row-group sizes from the rows this level streams, so a
+  // warm-start level fills the chip like a full pass
+  const int64_t n_total = level_rows(offsets, K, frac, min_rows);
   const int P = p + (intercept ? 1 : 0);
   const int NB = (P + kWideTile - 1) / kWideTile;
   const int TB = NB * (NB + 1) / 2;
@@ -297,6 +310,42 @@ int dlsa_last_fit_stats(dlsa_fit_stats* out) {
 }  // extern "C"
 
 namespace dlsa {
+
+// Rows a pass of phase `ph` streams: the rows (in this level's plan) of the
+// partitions whose phase is ph.  The partition phases are read back with the
+// per-iteration counters (stats only: rows_fp32 / rows_fp64).
+static std::vector<int64_t> plan_part_rows(const Plan& q, int K) {
+  std::vector<int64_t> r(K, 0);
+  for (int k = 0; k < K; ++k)
+    for (int c = q.part_chunk_begin[k]; c < q.part_chunk_begin[k + 1]; ++c) r[k] += q.chunk_rows[c];
+  return r;
+}
+static int64_t phase_rows(const std::vector<int64_t>& part_rows, const std::vector<int32_t>& phase,
+                          int ph) {
+  int64_t n = 0;
+  for (size_t k = 0; k < part_rows.size(); ++k)
+    if (phase[k] == ph) n += part_rows[k];
+  return n;
+}
+
+// DLSA_TRACE=1: per-iteration max |step| over all partitions (diagnostics;
+// copies theta and the last step to the host, so only for investigation)
+static hipError_t trace_iteration(int K, int P, const double* theta, const double* dprev,
+                                  size_t lvl, int it, const int* n_running) {
+  std::vector<double> th((size_t)K * P), dp((size_t)K * P);
+  hipError_t e = hipMemcpy(th.data(), theta, 8LL * K * P, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(dp.data(), dprev, 8LL * K * P, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return e;
+  double dmax = 0.0, tmax = 0.0;
+  for (size_t i = 0; i < th.size(); ++i) {
+    dmax = std::max(dmax, std::fabs(dp[i]));
+    tmax = std::max(tmax, std::fabs(th[i]));
+  }
+  fprintf(stderr,
+          "[dlsa trace] level %zu iter %d: max|step| %.3e max|theta| %.3e running f32 %d f64 %d\n",
+          lvl, it, dmax, tmax, n_running[0], n_running[1]);
+  return hipSuccess;
+}
 
 // Event timer of the fit's stream (record_timing only).  A pair of events
 // brackets every launch; the elapsed times are read after the fit's final
@@ -489,6 +538,7 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
       if (p) (void)hipHostFree(p);
     }
   } hfree{h_cnt};
+  std::vector<int32_t> h_phase(K, 0);
 
   int it = 0;
   for (size_t lvl = 0; lvl < plans.size(); ++lvl) {
@@ -497,14 +547,16 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
     DLSA_HIP_TRY(upload_plan(q.rows, L.off_r_row0, L.off_r_rows, L.off_r_part, d_rcb));
     DLSA_HIP_TRY(upload_plan(q.gram, L.off_g_row0, L.off_g_rows, L.off_g_part, d_gcb));
     wa.n_gchunks = q.gram.n_chunks;
-    int64_t rows = 0;
-    for (int c = 0; c < q.rows.n_chunks; ++c) rows += q.rows.chunk_rows[c];
+    const std::vector<int64_t> part_rows = plan_part_rows(q.rows, K);
     if (lvl > 0) {
       DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
       DLSA_HIP_TRY(launch_level_reset(K, P, start_phase, d_phase, status, d_llprev, d_bt, theta,
                                       d_cnt, stream));
       DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, stream));
-      DLSA_HIP_TRY(hipStreamSynchronize(stream));
+    }
+    DLSA_HIP_TRY(hipMemcpyAsync(h_phase.data(), d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
+    DLSA_HIP_TRY(hipStreamSynchronize(stream));
+    if (lvl > 0) {
       n_running[0] = h_cnt[0];
       n_running[1] = h_cnt[1];
     }
@@ -525,10 +577,10 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
             ph == PHASE_F64 ? &g_stats.ms_pass_fp64 : &g_stats.ms_pass_fp32));
         if (ph == PHASE_F64) {
           g_stats.passes_fp64++;
-          g_stats.rows_fp64 += rows;
+          g_stats.rows_fp64 += phase_rows(part_rows, h_phase, ph);
         } else {
           g_stats.passes_fp32++;
-          g_stats.rows_fp32 += rows;
+          g_stats.rows_fp32 += phase_rows(part_rows, h_phase, ph);
         }
       }
       DLSA_HIP_TRY(timed(&g_stats.ms_wide_assemble,
@@ -537,9 +589,12 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
       DLSA_HIP_TRY(timed(&g_stats.ms_solve,
                          [&] { return launch_wide_newton(sa, wa, d_rcb, d_H, K, stream); }));
       DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, stream));
+      DLSA_HIP_TRY(hipMemcpyAsync(h_phase.data(), d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
       DLSA_HIP_TRY(hipStreamSynchronize(stream));
       n_running[0] = h_cnt[0];
       n_running[1] = h_cnt[1];
+      if (getenv("DLSA_TRACE"))
+        DLSA_HIP_TRY(trace_iteration(K, P, theta, sa.delta_prev, lvl, it, n_running));
     }
   }
   g_stats.iterations = it;
@@ -670,12 +725,6 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
     }
   }
   plans.push_back(pl);
-  std::vector<int64_t> plan_rows;
-  for (const Plan& q : plans) {
-    int64_t rows = 0;
-    for (int c = 0; c < q.n_chunks; ++c) rows += q.chunk_rows[c];
-    plan_rows.push_back(rows);
-  }
 
   if (family == FAMILY_GAUSSIAN) max_iter = 1;  // closed form: one exact fp64 pass
   const int start_phase =
@@ -753,17 +802,22 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
   } hfree{h_cnt};
 
   const bool trace = getenv("DLSA_TRACE") != nullptr;
+  std::vector<int32_t> h_phase(K, 0);
   int it = 0;
   for (size_t lvl = 0; lvl < plans.size(); ++lvl) {
     const Plan& q = plans[lvl];
     const bool final_level = lvl + 1 == plans.size();
+    const std::vector<int64_t> part_rows = plan_part_rows(q, K);
     DLSA_HIP_TRY(upload(q));
     if (lvl > 0) {  // re-enter every running partition
       DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
       DLSA_HIP_TRY(launch_level_reset(K, P, start_phase, d_phase, status, d_llprev, d_bt, theta,
                                       d_cnt, stream));
       DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, stream));
-      DLSA_HIP_TRY(hipStreamSynchronize(stream));
+    }
+    DLSA_HIP_TRY(hipMemcpyAsync(h_phase.data(), d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
+    DLSA_HIP_TRY(hipStreamSynchronize(stream));
+    if (lvl > 0) {
       n_running[0] = h_cnt[0];
       n_running[1] = h_cnt[1];
     }
@@ -820,30 +874,20 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
       }));
       if (f64) {
         g_stats.passes_fp64++;
-        g_stats.rows_fp64 += plan_rows[lvl];
+        g_stats.rows_fp64 += phase_rows(part_rows, h_phase, ph);
       } else {
         g_stats.passes_fp32++;
-        g_stats.rows_fp32 += plan_rows[lvl];
+        g_stats.rows_fp32 += phase_rows(part_rows, h_phase, ph);
       }
     }
     DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
     DLSA_HIP_TRY(timed(&g_stats.ms_solve, [&] { return launch_newton_solve(sa, K, stream); }));
     DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, stream));
+    DLSA_HIP_TRY(hipMemcpyAsync(h_phase.data(), d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
     DLSA_HIP_TRY(hipStreamSynchronize(stream));
     n_running[0] = h_cnt[0];
     n_running[1] = h_cnt[1];
-    if (trace) {  // DLSA_TRACE=1: per-iteration max |step| over partitions (diagnostics)
-      std::vector<double> th((size_t)K * P), dp((size_t)K * P);
-      DLSA_HIP_TRY(hipMemcpy(th.data(), theta, 8LL * K * P, hipMemcpyDeviceToHost));
-      DLSA_HIP_TRY(hipMemcpy(dp.data(), d_dprev, 8LL * K * P, hipMemcpyDeviceToHost));
-      double dmax = 0.0, tmax = 0.0;
-      for (size_t e = 0; e < th.size(); ++e) {
-        dmax = std::max(dmax, std::fabs(dp[e]));
-        tmax = std::max(tmax, std::fabs(th[e]));
-      }
-      fprintf(stderr, "[dlsa trace] level %zu iter %d: max|step| %.3e max|theta| %.3e running f32 %d f64 %d\n",
-              lvl, it, dmax, tmax, n_running[0], n_running[1]);
-    }
+    if (trace) DLSA_HIP_TRY(trace_iteration(K, P, theta, d_dprev, lvl, it, n_running));
   }
   }
   g_stats.iterations = it;
