@@ -191,7 +191,12 @@ static void make_wide_plans(const int64_t* offsets, int K, int p, int intercept,
   const int NB = (P + kWideTile - 1) / kWideTile;
   const int TB = NB * (NB + 1) / 2;
   int rpc_row = (int)std::max<int64_t>(256, std::min<int64_t>(n_total / 2048, 16384));
-  int64_t groups = ((1024 + TB - 1) / TB + 7) / 8 * 8;
+  // >= 256 row groups: the all-tiles bf16 Gram pass runs wide_gram_all_groups(NB)
+  // workgroups per row group (4 at P > 384: 1024 in all) and the fp64 tiled
+  // pass TB per row group; measured at config 5 (p = 500): 64 / 128 / 256 row
+  // groups -> 183 / 188 / 177 ms per fit (fp64 pass 43.8 / 36.8 / 36.1 ms)
+  int64_t groups = (std::max<int64_t>(256, (1024 + TB - 1) / TB) + 7) / 8 * 8;
+  if (getenv("DLSA_WIDE_GRAM_TILED")) groups = ((1024 + TB - 1) / TB + 7) / 8 * 8;
   int rpc_gram = (int)std::max<int64_t>(1024, std::min<int64_t>((n_total + groups - 1) / groups,
                                                                 int64_t(1) << 24));
   if (rows_per_chunk > 0) rpc_row = rpc_gram = rows_per_chunk;

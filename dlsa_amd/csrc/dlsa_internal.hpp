@@ -124,6 +124,8 @@ struct WideArgs {
 hipError_t launch_wide_row(const WideArgs& a, bool standardize, int family, int n_chunks,
                            hipStream_t s);
 hipError_t launch_wide_gram(const WideArgs& a, bool standardize, bool f64, hipStream_t s);
+hipError_t launch_wide_gram_all(const WideArgs& a, bool standardize, hipStream_t s);
+int wide_gram_all_groups(int NB);  // workgroups per row group of the all-tiles bf16 pass
 hipError_t launch_wide_assemble(const WideArgs& a, const int32_t* gcb, double* Hfull, int K,
                                 hipStream_t s);
 hipError_t launch_wide_newton(const SolveArgs& sa, const WideArgs& wa, const int32_t* rcb,

@@ -24,6 +24,7 @@
 //                       update / convergence (same state machine as
 //                       newton_solve.hip).
 #include <math.h>
+#include <stdlib.h>
 
 #include "dlsa_internal.hpp"
 
@@ -439,6 +440,199 @@ __global__ __launch_bounds__(512, 1) void wide_gram_bf16_kernel(const WideArgs a
       }
 }
 
+
+// ---------------------------------------------------------------------------
+// bf16 Gram pass, one pass over a row group for ALL its tiles (approximate
+// Hessian of the MIXED mode).  The per-tile kernel above re-reads each row
+// once per 128 x 128 tile that needs it (5x at P = 500: L2/MALL-bound, 16 ms
+// per pass at config 5); here a workgroup streams its rows once:
+//   Z = bf16(sqrt(w) x),  H~ = Z^T Z   (positive semi-definite by construction)
+// per 32-row block: 512 threads load x (fp64, coalesced along the features),
+// scale, convert and write the feature-major image Z[PP][32] (96-byte feature
+// stride: conflict-free ds_read_b128 operand reads), one barrier, then each
+// wave runs one v_mfma_f32_16x16x32_bf16 per owned 16 x 16 lower-triangle
+// tile.  The fp32 accumulators of all NT16 (NT16 + 1) / 2 tiles must fit the
+// workgroup's registers: S workgroups share a row group, each owning a
+// contiguous range of the tiles (S = 2 / 4 above PP = 256 / 384; they run on
+// one XCD, so the repeated reads of the rows are L2 hits).  Output: the 128 x 128-tile
+// slab layout of wide_gram_kernel (wide_assemble_kernel reads the lower
+// triangle of diagonal tiles only).
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int ZS = 96;  // bytes per feature row of the Z image (32 rows of bf16 + pad)
+// 16x16 tiles of the lower triangle: 136 / 300 / 528 at NT16 = 16 / 24 / 32;
+// the accumulators of a group (4 VGPRs per tile per wave) stay <= ~150 VGPRs
+__host__ __device__ constexpr int zall_groups(int NT16) {
+  return NT16 > 24 ? 4 : (NT16 > 16 ? 2 : 1);
+}
+}  // namespace
+
+template <bool STD, int NT16>
+__global__ __launch_bounds__(512, 1) void wide_gram_all_bf16_kernel(const WideArgs a) {
+  constexpr int S = zall_groups(NT16);
+  constexpr int T = NT16 * (NT16 + 1) / 2;
+  constexpr int TG = (T + S - 1) / S;    // tiles per group
+  constexpr int TPW = (TG + 7) / 8;      // tiles per wave
+  constexpr int PP = 16 * NT16;
+  constexpr int ITEMS = PP * 4 / 512;    // (feature, 8-row group) items per thread
+  extern __shared__ __attribute__((aligned(16))) char zimg[];  // [2][PP][ZS]
+
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, j8 = bid >> 3;
+  const int sg = j8 % S, cl = j8 / S;
+  const int chunk = cl * 8 + xcd;  // the S groups of a row group on one XCD
+  if (chunk >= a.n_gchunks) return;
+  const int part = a.gc_part[chunk];
+  if (a.phase[part] != a.want_phase) return;  // workgroup-uniform
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int p = a.p, ic = a.intercept;
+  const int64_t row0 = a.gc_row0[chunk];
+  const int nrows = a.gc_rows[chunk];
+  const int nb = (nrows + 31) / 32;
+
+  // this wave's tiles (wave-uniform registers)
+  int tI[TPW], tJ[TPW];
+  bool tv[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const int t = sg * TG + wid * TPW + i;
+    tv[i] = (wid * TPW + i < TG) && t < T;
+    int I = 0;
+    while ((I + 1) * (I + 2) / 2 <= t) ++I;
+    tI[i] = __builtin_amdgcn_readfirstlane(tv[i] ? I : 0);
+    tJ[i] = __builtin_amdgcn_readfirstlane(tv[i] ? t - I * (I + 1) / 2 : 0);
+  }
+
+  // staging items: feature f = (tid + 512 m) % PP, rows 8 g .. 8 g + 7
+  int colx[ITEMS], fz[ITEMS], gz[ITEMS];
+  bool inx[ITEMS], onex[ITEMS];
+  double cx[ITEMS], sx[ITEMS];
+#pragma unroll
+  for (int m = 0; m < ITEMS; ++m) {
+    const int idx = tid + 512 * m;
+    const int f = idx % PP, g = idx / PP;
+    fz[m] = f;
+    gz[m] = g;
+    const int jj = f - ic;
+    inx[m] = jj >= 0 && jj < p;
+    onex[m] = ic && f == 0;
+    colx[m] = inx[m] ? jj : 0;
+    cx[m] = 0.0;
+    sx[m] = 1.0;
+    if constexpr (STD) {
+      if (inx[m]) {
+        cx[m] = a.center[jj];
+        sx[m] = 1.0 / a.scale[jj];
+      }
+    }
+  }
+
+  double xb[ITEMS][8];
+  auto load = [&](int b) {
+#pragma unroll
+    for (int m = 0; m < ITEMS; ++m)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        int r = 32 * b + 8 * gz[m] + e;
+        r = r < nrows ? r : nrows - 1;
+        xb[m][e] = a.X[(row0 + r) * (int64_t)p + colx[m]];
+      }
+  };
+  auto stage = [&](int b) {
+    char* img = zimg + (b & 1) * (PP * ZS);
+    // sqrt(w) of the block's 32 rows: lane l (< 32) holds row l, broadcast by
+    // v_readlane (the row of an item is wave-uniform); rows past the chunk: 0
+    const int rl = 32 * b + (lane & 31);
+    const float swl = rl < nrows ? sqrtf((float)a.w[row0 + rl]) : 0.f;
+#pragma unroll
+    for (int m = 0; m < ITEMS; ++m) {
+      bf16x8w z;
+      const int g8 = __builtin_amdgcn_readfirstlane(8 * gz[m]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float sw = __builtin_bit_cast(
+            float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, swl), g8 + e));
+        double v = inx[m] ? xb[m][e] : 0.0;
+        if constexpr (STD) v = (v - cx[m]) * sx[m];
+        if (onex[m]) v = 1.0;
+        float vf = (float)v;
+        asm volatile("" : "+v"(vf));  // keep f64 -> f32 -> bf16 (see irls_coop_impl.hpp)
+        z[e] = (__bf16)(vf * sw);
+      }
+      *(bf16x8w*)(img + fz[m] * ZS + 16 * gz[m]) = z;
+    }
+  };
+
+  f4w acc[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) acc[i] = f4w{0.f, 0.f, 0.f, 0.f};
+  const int fl = lane & 15, kg = lane >> 4;
+
+  if (nb > 0) load(0);
+  for (int b = 0; b < nb; ++b) {
+    stage(b);
+    if (b + 1 < nb) load(b + 1);  // in flight during the barrier and the MFMAs
+    __syncthreads();              // image b complete; every wave is past block b-1
+    const char* img = zimg + (b & 1) * (PP * ZS);
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) {
+      if (tv[i]) {  // wave-uniform
+        const bf16x8w av = *(const bf16x8w*)(img + (16 * tI[i] + fl) * ZS + 16 * kg);
+        const bf16x8w bv = *(const bf16x8w*)(img + (16 * tJ[i] + fl) * ZS + 16 * kg);
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[i], 0, 0, 0);
+      }
+    }
+  }
+
+  // C/D map of the f32 16x16 MFMAs: row = 4 (l >> 4) + r, column = l & 15
+  constexpr int NB = NT16 / 8;
+  constexpr int TB = NB * (NB + 1) / 2;
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    if (!tv[i]) continue;
+    const int I = tI[i], J = tJ[i];
+    const int I8 = I >> 3, J8 = J >> 3;
+    const int t128 = I8 * (I8 + 1) / 2 + J8;
+    double* G = a.slab_G + ((int64_t)chunk * TB + t128) * (GT * GT);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int il = 16 * (I & 7) + 4 * kg + r;
+      const int jl = 16 * (J & 7) + fl;
+      G[il * GT + jl] = (double)acc[i][r];
+    }
+  }
+}
+
+template <bool STD, int NT16>
+static hipError_t launch_gram_all_t(const WideArgs& a, hipStream_t s) {
+  auto kern = wide_gram_all_bf16_kernel<STD, NT16>;
+  static bool attr_set = false;
+  const int lds = 2 * 16 * NT16 * ZS;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int grid = ((a.n_gchunks + 7) / 8) * 8 * zall_groups(NT16);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, s, a);
+  return hipGetLastError();
+}
+
+// workgroups per row group of the all-tiles bf16 Gram pass (plan sizing)
+int wide_gram_all_groups(int NB) { return zall_groups(8 * NB); }
+
+hipError_t launch_wide_gram_all(const WideArgs& a, bool standardize, hipStream_t s) {
+  if (a.n_gchunks <= 0) return hipSuccess;
+  switch (a.NB) {
+    case 2: return standardize ? launch_gram_all_t<true, 16>(a, s) : launch_gram_all_t<false, 16>(a, s);
+    case 3: return standardize ? launch_gram_all_t<true, 24>(a, s) : launch_gram_all_t<false, 24>(a, s);
+    case 4: return standardize ? launch_gram_all_t<true, 32>(a, s) : launch_gram_all_t<false, 32>(a, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // assemble: H[k] (PP x PP, both triangles, padding = identity) = sum of the
 // row-group partials of partition k in row-group order.  grid (TB, K).
@@ -816,6 +1010,7 @@ hipError_t launch_wide_gram(const WideArgs& a, bool standardize, bool f64, hipSt
   const int TB = a.NB * (a.NB + 1) / 2;
   const int grid = ((a.n_gchunks + 7) / 8) * 8 * TB;
   if (!f64) {
+    if (!getenv("DLSA_WIDE_GRAM_TILED")) return launch_wide_gram_all(a, standardize, s);
     if (standardize)
       hipLaunchKernelGGL(wide_gram_bf16_kernel<true>, dim3(grid), dim3(512), 0, s, a);
     else
