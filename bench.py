@@ -116,6 +116,9 @@ def main():
     ap.add_argument("--cpu-parts", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=2019)
+    ap.add_argument("--layout", default="codes", choices=["codes", "dense"],
+                    help="config 3: categorical-code layout (LDS-histogram pass) or the dense "
+                         "dummy-coded design")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
     for key, v in (("n", args.n), ("p", args.p), ("K", args.partitions)):
@@ -137,7 +140,8 @@ def main():
     from dlsa_amd import _hip
     from dlsa_amd.dlsa import reduce_partitions_device, split_reduced, wlse
     from dlsa_amd.lsa import lars_lsa
-    from dlsa_amd.models import (logistic_model_batched, ols_model_batched, simulate_dummy_design,
+    from dlsa_amd.models import (logistic_model_batched, logistic_model_batched_categorical,
+                                 ols_model_batched, simulate_categorical, simulate_dummy_design,
                                  simulate_logistic_device)
 
     n, p, K, family = cfg["n"], cfg["p"], cfg["K"], cfg["family"]
@@ -146,7 +150,11 @@ def main():
     P = p + int(fit_intercept)
     wide = P > _hip.MAX_P_FUSED
     offsets = (np.arange(K + 1, dtype=np.int64) * n) // K
-    if data == "dummy":
+    codes_layout = data == "dummy" and args.layout == "codes"
+    if codes_layout:
+        X, codes, y, levels = simulate_categorical(n, seed=args.seed + rank, device=dev)
+        assert X.shape[1] + int((levels - 1).sum()) == p
+    elif data == "dummy":
         X, y = simulate_dummy_design(n, seed=args.seed + rank, device=dev)
         assert X.shape[1] == p
     else:
@@ -163,6 +171,10 @@ def main():
         nonlocal ws
         if family == "ols":
             fit = ols_model_batched(X, y, offsets, record_timing=record, device=dev)
+        elif codes_layout:
+            fit = logistic_model_batched_categorical(X, codes, y, offsets, levels,
+                                                     fit_intercept=fit_intercept, tol=args.tol,
+                                                     record_timing=record, device=dev)
         else:
             fit = logistic_model_batched(X, y, offsets, fit_intercept=fit_intercept,
                                          hessian=args.hessian, tol=args.tol,
@@ -203,9 +215,27 @@ def main():
     # (HIP events recorded on the fit's stream around every launch)
     tot = lambda key: sum(s[key] for s in stats_acc)  # noqa: E731
     row_bytes = 8 * p + 8                        # X row + y, read once per pass
+    if codes_layout:                             # numeric columns + uint8 codes + y
+        row_bytes = 8 * X.shape[1] + codes.shape[1] + 8
     alg_flops_row = P * (P + 1) + 4 * P + 20     # symmetric X^T W X + X.b, X^T r
     kern = {}
-    if wide:
+    if codes_layout:
+        ms64, n64, rows64 = tot("ms_pass_fp64"), tot("passes_fp64"), tot("rows_fp64")
+        kern["cat_pass_kernel"] = {
+            "launches_per_step": n64 / args.steps, "ms_per_step": ms64 / args.steps,
+            "avg_launch_ms": ms64 / n64, "rows_per_launch": rows64 / n64,
+            "GBps": rows64 * row_bytes / (ms64 * 1e-3) / 1e9,
+            "Grows_per_s": rows64 / (ms64 * 1e-3) / 1e9}
+        kern["newton_solve"] = {"ms_per_step": tot("ms_solve") / args.steps}
+        achieved = rows64 * row_bytes / (ms64 * 1e-3) / 1e9
+        roof = {"kernel": "cat_pass_kernel (categorical codes, one-hot blocks as fp64 LDS "
+                          "histograms)", "bound": "hbm", "achieved": achieved,
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                "traffic": None, "algorithmic_bytes_per_launch": rows64 * row_bytes / n64,
+                "avg_launch_ms": ms64 / n64,
+                "note": "bytes/row = 8 q + F + 8 (codes layout); the kernel issues ~47 fp64 "
+                        "LDS atomics per row, which bound it before HBM"}
+    elif wide:
         NB = (P + 127) // 128
         gram_flops_row = NB * (NB + 1) // 2 * 128 * 128 * 2  # issued MFMA work per row
         n32, n64 = tot("passes_fp32"), tot("passes_fp64")
@@ -291,13 +321,16 @@ def main():
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
         "data": ("synthetic airline-like: 9 U(-1/2,1/2) numeric + dummies of 5 skewed factors "
                  "(12/7/20/69/69 levels, baseline dropped), y~Bernoulli(sigmoid(-0.3+X beta*)); "
-                 "torch generator in HBM (not timed)") if data == "dummy" else
+                 "torch generator in HBM (not timed); layout: " +
+                 ("uint8 level codes + numeric columns" if codes_layout else
+                  "dense dummy design")) if data == "dummy" else
                 "synthetic: X~U(-1/2,1/2), beta*=1 on first floor(0.4p) cols, y~Bernoulli"
                 "(sigmoid(X beta*)); counter-based generator in HBM (not timed)",
         "config": {"workload": cfg["name"] + " + DLSA combine + LARS/DBIC",
                    "n_rows_per_gpu": n, "p": p, "P": P, "fit_intercept": fit_intercept,
                    "partitions_per_gpu": K,
-                   "family": family, "hessian": args.hessian if family == "logistic" else "fp64",
+                   **({"layout": args.layout} if data == "dummy" else {}),
+                   "family": family, "hessian": args.hessian if family == "logistic" and not codes_layout else "fp64",
                    "tol": args.tol,
                    "parallelism": f"dp{world} (partitions sharded; 1 RCCL all-reduce of P^2+2P+1 fp64)"},
         "roofline": roof,

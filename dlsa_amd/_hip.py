@@ -17,7 +17,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libdlsa_hip.so")
 
 DLSA_OK = 0
-STATUS_NAMES = {0: "ok", 1: "maxiter", 2: "singular", 3: "empty", 4: "nonfinite"}
+STATUS_NAMES = {0: "ok", 1: "maxiter", 2: "singular", 3: "empty", 4: "nonfinite", 5: "missing_level"}
 HESSIAN_MIXED = 0
 HESSIAN_FP64 = 1
 HESSIAN_MIXED_F32 = 2
@@ -85,6 +85,10 @@ SIGNATURES = {
          _P]),
     "dlsa_logistic_loglik_batched": (
         ctypes.c_int, [_P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _I32, _P, _P]),
+    "dlsa_logistic_fit_categorical": (
+        ctypes.c_int,
+        [_P, _P, _P, _P, _I32, _I32, _I32, _P, _I32, _P, _P, _I32, _F64, _P, _P, _P, _P, _P, _P,
+         ctypes.POINTER(FitOptions), _P]),
     "dlsa_last_fit_stats": (ctypes.c_int, [ctypes.POINTER(FitStats)]),
     "dlsa_reduce_partitions": (ctypes.c_int, [_P, _P, _P, _I32, _I32, _P, _P]),
     "dlsa_simulate_logistic": (ctypes.c_int, [_P, _P, _I64, _I32, ctypes.c_uint64, _I64, _P]),

@@ -906,6 +906,315 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
   return DLSA_OK;
 }
 
+// ---- categorical-code fit (cat_pass.hip) ---------------------------------
+// LDS layout of the histograms: replicas so that a frequent level does not
+// serialise the lanes of a wave on one address (nd: <= 128 slots per factor,
+// pairs: <= 512 cells), shrunk until the workgroup fits 160 KB.
+static bool cat_layout(CatArgs& a, const int32_t* levels) {
+  const int Qw = a.q + 1;
+  int nd_cap = 128, pr_cap = 512;
+  for (int attempt = 0; attempt < 12; ++attempt) {
+    int64_t o = 0;
+    for (int f = 0; f < a.F; ++f) {
+      const int nl = levels[f] - 1;
+      int R = 1;
+      while (R < 16 && nl * R * 2 <= nd_cap) R *= 2;
+      a.nlev[f] = nl;
+      a.nd_rep[f] = R;
+      a.nd_off[f] = (int32_t)o;
+      o += (int64_t)R * nl * Qw;
+    }
+    for (int f = 0; f < a.F; ++f) {
+      a.g_off[f] = (int32_t)o;
+      o += (int64_t)a.nd_rep[f] * a.nlev[f];
+    }
+    for (int f = 0; f < a.F; ++f)
+      for (int g = f + 1; g < a.F; ++g) {
+        const int pi = f * a.F - f * (f + 1) / 2 + (g - f - 1);
+        const int cells = a.nlev[f] * a.nlev[g];
+        int R = 1;
+        while (R < 8 && cells * R * 2 <= pr_cap) R *= 2;
+        a.pr_rep[pi] = R;
+        a.pr_off[pi] = (int32_t)o;
+        o += (int64_t)R * cells;
+      }
+    a.hist_doubles = (int32_t)std::min<int64_t>(o, INT32_MAX);
+    if (cat_lds_bytes(a) + kCatStaticLds <= 160 * 1024) return true;
+    if (nd_cap == 1 && pr_cap == 1) break;
+    nd_cap = std::max(1, nd_cap / 2);
+    pr_cap = std::max(1, pr_cap / 2);
+  }
+  return false;
+}
+
+static int fit_categorical(const double* Xn, const uint8_t* codes, const double* y,
+                           const int64_t* offsets, int32_t K, int32_t q, int32_t F,
+                           const int32_t* levels, int32_t fit_intercept, const double* center,
+                           const double* scale, int32_t max_iter, double tol, double* theta,
+                           double* sig_inv, double* sig_inv_theta, double* loglik, int32_t* iters,
+                           int32_t* status, const dlsa_fit_options* opt_in, void* stream_) {
+  const auto t_start = std::chrono::steady_clock::now();
+  g_last_error.clear();
+  memset(&g_stats, 0, sizeof(g_stats));
+  hipStream_t stream = (hipStream_t)stream_;
+  dlsa_fit_options opt;
+  if (opt_in)
+    opt = *opt_in;
+  else
+    dlsa_fit_options_default(&opt);
+  int rc = check_offsets(offsets, K);
+  if (rc != DLSA_OK) return rc;
+  if (q < 0 || F < 0 || F > kCatMaxFactors || (F > 0 && !levels)) {
+    set_error("need 0 <= q, 0 <= F <= 16 and a host levels[F] array");
+    return DLSA_E_INVALID;
+  }
+  int D = 0;
+  for (int f = 0; f < F; ++f) {
+    if (levels[f] < 1 || levels[f] > 256) {
+      set_error("levels[" + std::to_string(f) + "] must be in 1..256 (uint8 codes)");
+      return DLSA_E_INVALID;
+    }
+    D += levels[f] - 1;
+  }
+  const int ic = fit_intercept ? 1 : 0;
+  const int P = ic + q + D;
+  if (P < 1 || P > DLSA_MAX_P_FUSED || ic + q > kCatQMax) {
+    set_error("categorical fit needs 1 <= P = intercept + q + sum(levels - 1) <= " +
+              std::to_string(DLSA_MAX_P_FUSED) + " and intercept + q <= " +
+              std::to_string(kCatQMax) + " (got P = " + std::to_string(P) + ")");
+    return DLSA_E_UNSUPPORTED;
+  }
+  if ((center == nullptr) != (scale == nullptr)) {
+    set_error("center and scale must both be given or both be NULL");
+    return DLSA_E_INVALID;
+  }
+  if (!theta || !sig_inv || !sig_inv_theta || !loglik || !iters || !status) {
+    set_error("null output pointer");
+    return DLSA_E_INVALID;
+  }
+  const int64_t n_total = offsets[K];
+  if (n_total > 0 && (!y || (q > 0 && !Xn) || (F > 0 && !codes))) {
+    set_error("null Xn, codes or y");
+    return DLSA_E_INVALID;
+  }
+  if (max_iter < 1) max_iter = 1;
+  if (!(tol > 0)) tol = 1e-10;
+
+  CatArgs ca;
+  memset(&ca, 0, sizeof(ca));
+  ca.q = q;
+  ca.F = F;
+  ca.P = P;
+  ca.intercept = ic;
+  int d = ic + q;
+  for (int f = 0; f < F; ++f) {
+    ca.doff[f] = d;
+    d += levels[f] - 1;
+  }
+  if (!cat_layout(ca, levels)) {
+    set_error("categorical histograms do not fit the 160 KB LDS of a workgroup (P = " +
+              std::to_string(P) + ")");
+    return DLSA_E_UNSUPPORTED;
+  }
+
+  // chunks: ~2 workgroups (512 threads, one per CU at this LDS size) per CU,
+  // sized from the rows each level streams
+  auto cat_rpc = [&](int64_t rows) {
+    if (opt.rows_per_chunk > 0) return (int)opt.rows_per_chunk;
+    return (int)std::max<int64_t>(2048, std::min<int64_t>(rows / 512, 1 << 20));
+  };
+  std::vector<Plan> plans;
+  if (opt.warm_start) {
+    const int64_t min_rows = std::max<int64_t>(2048, 64LL * P);
+    for (double frac : {1.0 / 16.0, 1.0 / 4.0}) {
+      Plan qn;
+      const int64_t lr = level_rows(offsets, K, frac, min_rows);
+      make_plan(offsets, K, P - ic, ic, cat_rpc(lr), qn, frac, min_rows);
+      if (lr <= n_total / 2 && qn.n_chunks > 0) plans.push_back(std::move(qn));
+    }
+  }
+  {
+    Plan full;
+    make_plan(offsets, K, P - ic, ic, cat_rpc(n_total), full);
+    plans.push_back(std::move(full));
+  }
+  const Plan& pl = plans.back();
+  int max_chunks = 0;
+  for (const Plan& qn : plans) max_chunks = std::max(max_chunks, qn.n_chunks);
+  Plan sizing = pl;
+  sizing.n_chunks = max_chunks;
+  const Layout L = make_layout(sizing, K);
+  const int64_t off_counts = align_up(L.total, 256);
+  const int64_t off_bad = align_up(off_counts + 4LL * std::max(pl.n_chunks, 1) * std::max(D, 1), 256);
+  const int64_t off_badp = align_up(off_bad + 4LL * std::max(pl.n_chunks, 1), 256);
+  const int64_t total = align_up(off_badp + 4LL * K, 256);
+  g_stats.n_chunks = pl.n_chunks;
+
+  char* ws = (char*)opt.workspace;
+  bool owned = false;
+  if (!ws || opt.workspace_bytes < total) {
+    DLSA_HIP_TRY(hipMallocAsync((void**)&ws, total, stream));
+    owned = true;
+  }
+  struct Free {
+    char* p;
+    bool own;
+    hipStream_t s;
+    ~Free() {
+      if (own && p) (void)hipFreeAsync(p, s);
+    }
+  } freer{ws, owned, stream};
+  auto at = [&](int64_t off) { return (void*)(ws + off); };
+  int64_t* d_row0 = (int64_t*)at(L.off_row0);
+  int32_t* d_rows = (int32_t*)at(L.off_rows);
+  int32_t* d_part = (int32_t*)at(L.off_part);
+  int32_t* d_pcb = (int32_t*)at(L.off_pcb);
+  int64_t* d_offsets = (int64_t*)at(L.off_offsets);
+  int32_t* d_phase = (int32_t*)at(L.off_phase);
+  int32_t* d_bt = (int32_t*)at(L.off_bt);
+  double* d_llprev = (double*)at(L.off_llprev);
+  int32_t* d_cnt = (int32_t*)at(L.off_counters);
+  int32_t* d_counts = (int32_t*)at(off_counts);
+  int32_t* d_bad = (int32_t*)at(off_bad);
+  int32_t* d_badp = (int32_t*)at(off_badp);
+
+  auto upload = [&](const Plan& qn) -> hipError_t {
+    hipError_t e = hipSuccess;
+    if (qn.n_chunks > 0) {
+      e = hipMemcpyAsync(d_row0, qn.chunk_row0.data(), 8LL * qn.n_chunks, hipMemcpyHostToDevice,
+                         stream);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(d_rows, qn.chunk_rows.data(), 4LL * qn.n_chunks,
+                           hipMemcpyHostToDevice, stream);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(d_part, qn.chunk_part.data(), 4LL * qn.n_chunks,
+                           hipMemcpyHostToDevice, stream);
+    }
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(d_pcb, qn.part_chunk_begin.data(), 4LL * (K + 1),
+                         hipMemcpyHostToDevice, stream);
+    return e;
+  };
+  DLSA_HIP_TRY(hipMemcpyAsync(d_offsets, offsets, 8LL * (K + 1), hipMemcpyHostToDevice, stream));
+  DLSA_HIP_TRY(launch_fit_init(d_offsets, K, P, PHASE_F64, theta, d_phase, d_bt, iters, status,
+                               d_llprev, sig_inv, loglik, stream));
+
+  ca.Xn = Xn;
+  ca.codes = codes;
+  ca.y = y;
+  ca.chunk_row0 = d_row0;
+  ca.chunk_rows = d_rows;
+  ca.chunk_part = d_part;
+  ca.phase = d_phase;
+  ca.theta = theta;
+  ca.center = center;
+  ca.scale = scale;
+  ca.slab_H = (double*)at(L.off_slabH);
+  ca.slab_g = (double*)at(L.off_slabg);
+  ca.slab_ll = (double*)at(L.off_slabll);
+  ca.NT = pl.NT;
+  ca.want_phase = PHASE_F64;
+
+  // level presence over all rows: partitions missing a level -> zero frame;
+  // invalid codes fail the call
+  std::vector<int32_t> h_phase(K, 0), h_badp(K, 0);
+  DLSA_HIP_TRY(upload(pl));
+  if (D > 0) {
+    DLSA_HIP_TRY(launch_cat_presence(ca, pl.n_chunks, d_counts, d_bad, stream));
+    DLSA_HIP_TRY(launch_cat_mark(ca, d_pcb, d_counts, d_bad, K, d_phase, status, d_badp, stream));
+    DLSA_HIP_TRY(hipMemcpyAsync(h_badp.data(), d_badp, 4LL * K, hipMemcpyDeviceToHost, stream));
+  }
+  DLSA_HIP_TRY(hipMemcpyAsync(h_phase.data(), d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
+  DLSA_HIP_TRY(hipStreamSynchronize(stream));
+  for (int k = 0; k < K; ++k)
+    if (h_badp[k]) {
+      set_error("partition " + std::to_string(k) + ": " + std::to_string(h_badp[k]) +
+                " level codes >= levels[f]");
+      return DLSA_E_INVALID;
+    }
+  int n_running = 0;
+  for (int k = 0; k < K; ++k) n_running += h_phase[k] == PHASE_F64;
+
+  SolveArgs sa;
+  memset(&sa, 0, sizeof(sa));
+  sa.part_chunk_begin = d_pcb;
+  sa.slab_H = ca.slab_H;
+  sa.slab_g = ca.slab_g;
+  sa.slab_ll = ca.slab_ll;
+  sa.theta = theta;
+  sa.theta_prev = (double*)at(L.off_thprev);
+  sa.delta_prev = (double*)at(L.off_dprev);
+  sa.ll_prev = d_llprev;
+  sa.phase = d_phase;
+  sa.backtracks = d_bt;
+  sa.iters = iters;
+  sa.status = status;
+  sa.counters = d_cnt;
+  sa.sig_inv = sig_inv;
+  sa.loglik = loglik;
+  sa.P = P;
+  sa.NT = pl.NT;
+  sa.family = FAMILY_LOGISTIC;
+  sa.tol = tol;
+
+  const bool standardize = center != nullptr;
+  StreamTimer timed{stream, opt.record_timing != 0};
+  int32_t* h_cnt = nullptr;
+  DLSA_HIP_TRY(hipHostMalloc((void**)&h_cnt, 16, hipHostMallocDefault));
+  struct HFree {
+    int32_t* p;
+    ~HFree() {
+      if (p) (void)hipHostFree(p);
+    }
+  } hfree{h_cnt};
+  const bool trace = getenv("DLSA_TRACE") != nullptr;
+
+  int it = 0;
+  for (size_t lvl = 0; lvl < plans.size(); ++lvl) {
+    const Plan& qn = plans[lvl];
+    const bool final_level = lvl + 1 == plans.size();
+    const std::vector<int64_t> part_rows = plan_part_rows(qn, K);
+    DLSA_HIP_TRY(upload(qn));
+    if (lvl > 0) {
+      DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
+      DLSA_HIP_TRY(launch_level_reset(K, P, PHASE_F64, d_phase, status, d_llprev, d_bt, theta,
+                                      d_cnt, stream));
+      DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, stream));
+      DLSA_HIP_TRY(hipMemcpyAsync(h_phase.data(), d_phase, 4LL * K, hipMemcpyDeviceToHost,
+                                  stream));
+      DLSA_HIP_TRY(hipStreamSynchronize(stream));
+      n_running = h_cnt[0] + h_cnt[1];
+    }
+    sa.subsample = final_level ? 0 : 1;
+    sa.level_tol = 0.1;
+    sa.switch_tol = 0.0;
+    const int it_end = final_level ? max_iter : std::min(max_iter, it + 10);
+    for (; it < it_end && n_running > 0 && qn.n_chunks > 0; ++it) {
+      DLSA_HIP_TRY(timed(&g_stats.ms_pass_fp64,
+                         [&] { return launch_cat_pass(ca, standardize, qn.n_chunks, stream); }));
+      g_stats.passes_fp64++;
+      g_stats.rows_fp64 += phase_rows(part_rows, h_phase, PHASE_F64);
+      DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
+      DLSA_HIP_TRY(timed(&g_stats.ms_solve, [&] { return launch_newton_solve(sa, K, stream); }));
+      DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, stream));
+      DLSA_HIP_TRY(hipMemcpyAsync(h_phase.data(), d_phase, 4LL * K, hipMemcpyDeviceToHost,
+                                  stream));
+      DLSA_HIP_TRY(hipStreamSynchronize(stream));
+      n_running = h_cnt[0] + h_cnt[1];
+      int nr[2] = {h_cnt[0], h_cnt[1]};
+      if (trace) DLSA_HIP_TRY(trace_iteration(K, P, theta, sa.delta_prev, lvl, it, nr));
+    }
+  }
+  g_stats.iterations = it;
+  DLSA_HIP_TRY(launch_fit_finalize(K, P, theta, sig_inv, sig_inv_theta, status, stream));
+  DLSA_HIP_TRY(hipStreamSynchronize(stream));
+  g_stats.ms_total =
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start)
+          .count();
+  DLSA_HIP_TRY(timed.flush());
+  return DLSA_OK;
+}
+
 }  // namespace dlsa
 
 extern "C" {
@@ -918,6 +1227,18 @@ int dlsa_logistic_fit_batched_ex(const double* X, const double* y, const int64_t
                                  int32_t* status, const dlsa_fit_options* opt, void* stream) {
   return fit_impl(FAMILY_LOGISTIC, X, y, offsets, K, p, fit_intercept, center, scale, max_iter,
                   tol, theta, sig_inv, sig_inv_theta, loglik, iters, status, opt, stream);
+}
+
+int dlsa_logistic_fit_categorical(const double* Xn, const uint8_t* codes, const double* y,
+                                  const int64_t* offsets, int32_t K, int32_t q, int32_t F,
+                                  const int32_t* levels, int32_t fit_intercept,
+                                  const double* center, const double* scale, int32_t max_iter,
+                                  double tol, double* theta, double* sig_inv,
+                                  double* sig_inv_theta, double* loglik, int32_t* iters,
+                                  int32_t* status, const dlsa_fit_options* opt, void* stream) {
+  return fit_categorical(Xn, codes, y, offsets, K, q, F, levels, fit_intercept, center, scale,
+                         max_iter, tol, theta, sig_inv, sig_inv_theta, loglik, iters, status, opt,
+                         stream);
 }
 
 int dlsa_ols_fit_batched(const double* X, const double* y, const int64_t* offsets, int32_t K,

@@ -1,0 +1,408 @@
+// Categorical-code IRLS pass (BASELINE config 3).
+//
+// The reference dummy-encodes every factor on the host (dlsa/models.py:56-91:
+// pd.get_dummies, baseline levels dropped, a chunk missing a selected level
+// -> an all-zero frame) and then fits a dense n_k x p design.  Here a row is
+// stored as q fp64 numeric columns + F one-byte level codes + y
+// (8q + F + 8 bytes: 85 B at the airline shape instead of 1464 B dense), and
+// the one-hot blocks of X^T W X are weighted histograms:
+//
+//   numeric x numeric            dense, per-thread registers (QN <= 16)
+//   dummy (f,l) x numeric i      sum_{code_f = l} w x_i        LDS histogram
+//   dummy (f,l) x dummy (f,l)    sum_{code_f = l} w            (same, x = 1)
+//   dummy (f,l) x dummy (f,l')   0 (one-hot within a factor)
+//   dummy (f,l) x dummy (g,m)    sum_{code_f = l, code_g = m} w   2-D histogram
+//   gradient dummy (f,l)         sum_{code_f = l} (y - mu)
+//
+// All sums are fp64 (ds_add_f64): the Hessian is exact, so every pass is an
+// fp64 Newton pass and its H is Sig_inv.  Low-cardinality factors and pairs
+// keep several histogram replicas (lane & (R-1)) so the lanes of a wave that
+// share a frequent level do not serialise on one LDS address.  The order of
+// the fp64 additions inside a chunk follows the hardware's atomic order
+// (last-bit run-to-run differences; the chunk partials are then summed in a
+// fixed order).
+//
+// Parameter order: [intercept] [q numeric] [factor 0: levels 1..L_0-1] ...
+// -- the reference's column order (sorted numeric names, then each factor's
+// sorted dummy names, models.py:70-79) when the host encodes codes in sorted
+// dummy-name order (dlsa_amd.models.encode_categorical).
+//
+// The pass writes the same per-chunk partial slab (lower-triangle 16x16
+// tiles, gradient, log-likelihood) as the dense fused pass, so the Newton
+// solve, warm-start levels and phases are shared (capi.hip).
+#include <math.h>
+
+#include "dlsa_internal.hpp"
+
+namespace dlsa {
+
+__device__ __forceinline__ void lds_add(double* p, double v) {
+  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// pair index of factors f < g among F
+__host__ __device__ __forceinline__ int cat_pair(int f, int g, int F) {
+  return f * F - f * (f + 1) / 2 + (g - f - 1);
+}
+
+template <int QN, int FM, int NTHR, bool STD>
+__global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  constexpr int NW = NTHR / 64;
+  constexpr int NTRI = QN * (QN + 1) / 2;
+  constexpr int NR = NTRI + QN + 1;  // reduced register values: H block, gradient, ll
+  const int chunk = blockIdx.x;
+  const int part = a.chunk_part[chunk];
+  if (a.phase[part] != a.want_phase) return;  // workgroup-uniform
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int q = a.q, F = a.F, P = a.P, ic = a.intercept;
+  const int Qn = ic + q, Qw = q + 1;
+  double* hist = sm;                       // a.hist_doubles
+  double* th = sm + a.hist_doubles;        // kCatPMax: theta of this partition
+  double* stdv = th + kCatPMax;            // 2 x kCatQMax: center, 1 / scale
+  double* red = stdv + 2 * kCatQMax;       // NW x NR, then NR final sums
+
+  // factor / pair tables in LDS: re-read (broadcast) every row instead of
+  // pinning ~100 loop-invariant values in registers
+  __shared__ int32_t tb[5 * kCatMaxFactors + 2 * kCatMaxPairs];
+  int32_t* t_nlev = tb;
+  int32_t* t_doff = tb + kCatMaxFactors;
+  int32_t* t_ndoff = tb + 2 * kCatMaxFactors;
+  int32_t* t_ndrep = tb + 3 * kCatMaxFactors;
+  int32_t* t_goff = tb + 4 * kCatMaxFactors;
+  int32_t* t_proff = tb + 5 * kCatMaxFactors;
+  int32_t* t_prrep = t_proff + kCatMaxPairs;
+  for (int i = tid; i < kCatMaxFactors; i += NTHR) {
+    t_nlev[i] = a.nlev[i];
+    t_doff[i] = a.doff[i];
+    t_ndoff[i] = a.nd_off[i];
+    t_ndrep[i] = a.nd_rep[i] - 1;  // replica mask
+    t_goff[i] = a.g_off[i];
+  }
+  for (int i = tid; i < kCatMaxPairs; i += NTHR) {
+    t_proff[i] = a.pr_off[i];
+    t_prrep[i] = a.pr_rep[i] - 1;
+  }
+  for (int i = tid; i < a.hist_doubles; i += NTHR) hist[i] = 0.0;
+  for (int i = tid; i < kCatPMax; i += NTHR) th[i] = i < P ? a.theta[(int64_t)part * P + i] : 0.0;
+  if (STD && tid < kCatQMax) {
+    stdv[tid] = tid < q ? a.center[tid] : 0.0;
+    stdv[kCatQMax + tid] = tid < q ? 1.0 / a.scale[tid] : 1.0;
+  }
+  __syncthreads();
+
+  const int64_t row0 = a.chunk_row0[chunk];
+  const int nrows = a.chunk_rows[chunk];
+  double hacc[NTRI], gacc[QN], llacc = 0.0;
+#pragma unroll
+  for (int i = 0; i < NTRI; ++i) hacc[i] = 0.0;
+#pragma unroll
+  for (int i = 0; i < QN; ++i) gacc[i] = 0.0;
+
+  for (int r = tid; r < nrows; r += NTHR) {
+    const int64_t row = row0 + r;
+    const double* xr = a.Xn + row * q;
+    const uint8_t* cr = a.codes + row * F;
+    // parameter-order numeric vector: [1 if intercept] x_0 .. x_{q-1} (standardised)
+    double xv[QN];
+#pragma unroll
+    for (int i = 0; i < QN; ++i) {
+      const int j = i - ic;
+      double v = 0.0;
+      if (i < Qn) {
+        if (j < 0) {
+          v = 1.0;
+        } else {
+          v = xr[j];
+          if constexpr (STD) v = (v - stdv[j]) * stdv[kCatQMax + j];
+        }
+      }
+      xv[i] = v;
+    }
+    int cv[FM];
+#pragma unroll
+    for (int f = 0; f < FM; ++f) cv[f] = f < F ? (int)cr[f] : 0;
+
+    double e0 = 0.0, e1 = 0.0;
+#pragma unroll
+    for (int i = 0; i < QN; ++i) {
+      if (i & 1)
+        e1 = fma(xv[i], th[i], e1);
+      else
+        e0 = fma(xv[i], th[i], e0);
+    }
+#pragma unroll
+    for (int f = 0; f < FM; ++f)
+      if (f < F && cv[f] > 0) e0 += th[t_doff[f] + cv[f] - 1];
+    const double e = e0 + e1;
+    const double yv = a.y[row];
+    const double ea = exp(-fabs(e));
+    const double inv = 1.0 / (1.0 + ea);
+    const double mu = e >= 0.0 ? inv : ea * inv;
+    const double w = ea * inv * inv;  // mu (1 - mu), cancellation free
+    const double res = yv - mu;
+    llacc += yv * e - (fmax(e, 0.0) + log1p(ea));
+
+#pragma unroll
+    for (int i = 0; i < QN; ++i) {
+      gacc[i] = fma(res, xv[i], gacc[i]);
+      const double wxi = w * xv[i];
+#pragma unroll
+      for (int j = 0; j <= i; ++j) hacc[i * (i + 1) / 2 + j] = fma(wxi, xv[j], hacc[i * (i + 1) / 2 + j]);
+    }
+
+    // one-hot blocks: histograms in LDS
+#pragma unroll
+    for (int f = 0; f < FM; ++f) {
+      if (f < F && cv[f] > 0) {
+        const int slot = (lane & t_ndrep[f]) * t_nlev[f] + cv[f] - 1;
+        double* h = hist + t_ndoff[f] + slot * Qw;
+        lds_add(h, w);
+#pragma unroll
+        for (int i = 0; i < QN; ++i)  // numeric columns (register index compile-time)
+          if (i >= ic && i < Qn) lds_add(h + 1 + (i - ic), w * xv[i]);
+        lds_add(hist + t_goff[f] + slot, res);
+      }
+    }
+#pragma unroll
+    for (int f = 0; f < FM; ++f)
+#pragma unroll
+      for (int g = f + 1; g < FM; ++g) {
+        if (g < F && cv[f] > 0 && cv[g] > 0) {
+          const int pi = cat_pair(f, g, F);
+          const int rep = lane & t_prrep[pi];
+          lds_add(hist + t_proff[pi] + (rep * t_nlev[f] + cv[f] - 1) * t_nlev[g] + cv[g] - 1, w);
+        }
+      }
+  }
+
+  // ---- reduce the register blocks over the workgroup (fixed order) --------
+  auto wave_red = [&](double v) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) v += __shfl_xor(v, o);
+    return v;
+  };
+#pragma unroll
+  for (int i = 0; i < NTRI; ++i) {
+    const double v = wave_red(hacc[i]);
+    if (lane == 0) red[wid * NR + i] = v;
+  }
+#pragma unroll
+  for (int i = 0; i < QN; ++i) {
+    const double v = wave_red(gacc[i]);
+    if (lane == 0) red[wid * NR + NTRI + i] = v;
+  }
+  {
+    const double v = wave_red(llacc);
+    if (lane == 0) red[wid * NR + NTRI + QN] = v;
+  }
+  __syncthreads();
+  double* fin = red + NW * NR;
+  for (int i = tid; i < NR; i += NTHR) {
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) s += red[w * NR + i];
+    fin[i] = s;
+  }
+  __syncthreads();
+
+  // factor of dummy parameter index d (0-based among dummies)
+  auto factor_of = [&](int gi, int& lev) {
+    int f = 0;
+#pragma unroll
+    for (int g = 1; g < FM; ++g)
+      if (g < F && gi >= a.doff[g]) f = g;
+    lev = gi - a.doff[f];
+    return f;
+  };
+  auto nd_sum = [&](int f, int lev, int col) {
+    const int nl = a.nlev[f], R = a.nd_rep[f];
+    double s = 0.0;
+    for (int rp = 0; rp < R; ++rp) s += hist[a.nd_off[f] + (rp * nl + lev) * Qw + col];
+    return s;
+  };
+
+  // ---- epilogue: the partial slab in the dense pass's tile format ---------
+  const int NT = a.NT;
+  const int T = NT * (NT + 1) / 2;
+  double* dst = a.slab_H + (int64_t)chunk * T * 256;
+  for (int e = tid; e < T * 256; e += NTHR) {
+    const int t = e >> 8, pos = e & 255;
+    int I = 0;
+    while ((I + 1) * (I + 2) / 2 <= t) ++I;
+    const int J = t - I * (I + 1) / 2;
+    const int gi = 16 * I + (pos >> 4), gj = 16 * J + (pos & 15);
+    double v = 0.0;
+    if (gi < P && gj <= gi) {
+      if (gi < Qn) {
+        v = fin[gi * (gi + 1) / 2 + gj];
+      } else {
+        int li;
+        const int fi = factor_of(gi, li);
+        if (gj < Qn) {
+          v = nd_sum(fi, li, ic ? gj : gj + 1);
+        } else {
+          int lj;
+          const int fj = factor_of(gj, lj);
+          if (fj == fi) {
+            v = li == lj ? nd_sum(fi, li, 0) : 0.0;
+          } else {  // fj < fi
+            const int pi = cat_pair(fj, fi, F);
+            const int nli = a.nlev[fi], nlj = a.nlev[fj], R = a.pr_rep[pi];
+            for (int rp = 0; rp < R; ++rp)
+              v += hist[a.pr_off[pi] + (rp * nlj + lj) * nli + li];
+          }
+        }
+      }
+    }
+    dst[e] = v;
+  }
+  const int PP = 16 * NT;
+  for (int e = tid; e < PP; e += NTHR) {
+    double v = 0.0;
+    if (e < Qn) {
+      v = fin[NTRI + e];
+    } else if (e < P) {
+      int l;
+      const int f = factor_of(e, l);
+      const int nl = a.nlev[f], R = a.nd_rep[f];
+      for (int rp = 0; rp < R; ++rp) v += hist[a.g_off[f] + rp * nl + l];
+    }
+    a.slab_g[(int64_t)chunk * PP + e] = v;
+  }
+  if (tid == 0) a.slab_ll[chunk] = fin[NTRI + QN];
+}
+
+// Level presence per chunk: counts[chunk, d] = rows of the chunk whose code
+// selects dummy column d; bad[chunk] = codes outside 0..L_f-1.
+__global__ __launch_bounds__(256) void cat_presence_kernel(const CatArgs a, int32_t* counts,
+                                                           int32_t* bad) {
+  __shared__ int32_t cnt[kCatPMax + 1];
+  const int chunk = blockIdx.x, tid = threadIdx.x;
+  const int D = a.P - a.intercept - a.q;
+  const int F = a.F;
+  for (int i = tid; i <= kCatPMax; i += 256) cnt[i] = 0;
+  __syncthreads();
+  const int64_t row0 = a.chunk_row0[chunk];
+  const int nrows = a.chunk_rows[chunk];
+  const int doff0 = a.intercept + a.q;
+  for (int r = tid; r < nrows; r += 256) {
+    const uint8_t* cr = a.codes + (row0 + r) * F;
+    for (int f = 0; f < F; ++f) {
+      const int c = cr[f];
+      if (c > a.nlev[f])
+        atomicAdd(&cnt[kCatPMax], 1);
+      else if (c > 0)
+        atomicAdd(&cnt[a.doff[f] - doff0 + c - 1], 1);
+    }
+  }
+  __syncthreads();
+  for (int d = tid; d < D; d += 256) counts[(int64_t)chunk * D + d] = cnt[d];
+  if (tid == 0) bad[chunk] = cnt[kCatPMax];
+}
+
+// Per partition: a selected dummy level with no rows -> the reference's
+// all-zero frame (models.py:84-91): status MISSING_LEVEL, phase DONE, outputs
+// stay zero (fit_init zeroed theta / Sig_inv).  bad_part[k] = invalid codes.
+__global__ __launch_bounds__(256) void cat_mark_kernel(const CatArgs a, const int32_t* pcb,
+                                                       const int32_t* counts, const int32_t* bad,
+                                                       int32_t* phase, int32_t* status,
+                                                       int32_t* bad_part) {
+  __shared__ int32_t flag[2];
+  const int k = blockIdx.x, tid = threadIdx.x;
+  const int D = a.P - a.intercept - a.q;
+  if (tid < 2) flag[tid] = 0;
+  __syncthreads();
+  const int cb = pcb[k], ce = pcb[k + 1];
+  for (int d = tid; d < D; d += 256) {
+    int64_t s = 0;
+    for (int c = cb; c < ce; ++c) s += counts[(int64_t)c * D + d];
+    if (s == 0) flag[0] = 1;
+  }
+  int nb = 0;
+  for (int c = cb + tid; c < ce; c += 256) nb += bad[c];
+  if (nb) atomicAdd(&flag[1], nb);
+  __syncthreads();
+  if (tid == 0) {
+    bad_part[k] = flag[1];
+    if (ce > cb && flag[0] && status[k] == STATUS_RUNNING) {
+      status[k] = DLSA_STATUS_MISSING_LEVEL;
+      phase[k] = PHASE_DONE;
+    }
+  }
+}
+
+template <int QN, int FM, int NTHR, bool STD>
+static hipError_t launch_cat_t(const CatArgs& a, int n_chunks, size_t lds, hipStream_t s) {
+  auto kern = cat_pass_kernel<QN, FM, NTHR, STD>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    // dynamic + the kernel's static tables <= 160 KB
+    hipError_t e = hipFuncSetAttribute((const void*)kern,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       160 * 1024 - kCatStaticLds);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(n_chunks), dim3(NTHR), lds, s, a);
+  return hipGetLastError();
+}
+
+static int cat_qn(int Qn) { return Qn <= 4 ? 4 : Qn <= 8 ? 8 : Qn <= 10 ? 10 : Qn <= 12 ? 12 : 16; }
+static constexpr int cat_threads_t(int QN, int FM) {
+  return (QN <= 4 || (QN <= 10 && FM <= 8)) ? 512 : 256;
+}
+
+size_t cat_lds_bytes(const CatArgs& a) {
+  const int QN = cat_qn(a.intercept + a.q);
+  const int NR = QN * (QN + 1) / 2 + QN + 1;
+  const int NW = cat_threads_t(QN, a.F <= 8 ? 8 : 16) / 64;
+  return 8 * ((size_t)a.hist_doubles + kCatPMax + 2 * kCatQMax + (size_t)(NW + 1) * NR);
+}
+
+template <int QN>
+static hipError_t launch_cat_q(const CatArgs& a, bool std_, int n_chunks, size_t lds,
+                               hipStream_t s) {
+  // 512 threads while the register blocks fit 256 VGPRs (measured: QN <= 10
+  // with F <= 8), else 256 threads (512 VGPRs per lane)
+  if (a.F <= 8) {
+    constexpr int N8 = cat_threads_t(QN, 8);
+    return std_ ? launch_cat_t<QN, 8, N8, true>(a, n_chunks, lds, s)
+                : launch_cat_t<QN, 8, N8, false>(a, n_chunks, lds, s);
+  }
+  constexpr int N16 = cat_threads_t(QN, 16);
+  return std_ ? launch_cat_t<QN, 16, N16, true>(a, n_chunks, lds, s)
+              : launch_cat_t<QN, 16, N16, false>(a, n_chunks, lds, s);
+}
+
+hipError_t launch_cat_pass(const CatArgs& a, bool standardize, int n_chunks, hipStream_t s) {
+  if (n_chunks <= 0) return hipSuccess;
+  const size_t lds = cat_lds_bytes(a);
+  if (lds + kCatStaticLds > 160 * 1024 || a.F > kCatMaxFactors || a.q + a.intercept > kCatQMax)
+    return hipErrorInvalidValue;
+  switch (cat_qn(a.intercept + a.q)) {
+    case 4: return launch_cat_q<4>(a, standardize, n_chunks, lds, s);
+    case 8: return launch_cat_q<8>(a, standardize, n_chunks, lds, s);
+    case 10: return launch_cat_q<10>(a, standardize, n_chunks, lds, s);
+    case 12: return launch_cat_q<12>(a, standardize, n_chunks, lds, s);
+    default: return launch_cat_q<16>(a, standardize, n_chunks, lds, s);
+  }
+}
+
+hipError_t launch_cat_presence(const CatArgs& a, int n_chunks, int32_t* counts, int32_t* bad,
+                               hipStream_t s) {
+  if (n_chunks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(cat_presence_kernel, dim3(n_chunks), dim3(256), 0, s, a, counts, bad);
+  return hipGetLastError();
+}
+
+hipError_t launch_cat_mark(const CatArgs& a, const int32_t* pcb, const int32_t* counts,
+                           const int32_t* bad, int K, int32_t* phase, int32_t* status,
+                           int32_t* bad_part, hipStream_t s) {
+  hipLaunchKernelGGL(cat_mark_kernel, dim3(K), dim3(256), 0, s, a, pcb, counts, bad, phase,
+                     status, bad_part);
+  return hipGetLastError();
+}
+
+}  // namespace dlsa

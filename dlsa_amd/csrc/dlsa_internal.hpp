@@ -120,7 +120,46 @@ struct WideArgs {
   int32_t n_gchunks;
 };
 
+// Categorical-code pass (cat_pass.hip): q numeric fp64 columns + F uint8
+// level codes per row; the one-hot blocks of X^T W X are LDS histograms.
+constexpr int kCatMaxFactors = 16;
+constexpr int kCatMaxPairs = kCatMaxFactors * (kCatMaxFactors - 1) / 2;
+constexpr int kCatPMax = 192;  // P <= DLSA_MAX_P_FUSED (the Newton solve's limit)
+constexpr int kCatQMax = 16;   // intercept + numeric columns
+struct CatArgs {
+  const double* Xn;           // [n_total, q] numeric columns
+  const uint8_t* codes;       // [n_total, F] level codes (0 = baseline: no column)
+  const double* y;            // [n_total]
+  const int64_t* chunk_row0;
+  const int32_t* chunk_rows;
+  const int32_t* chunk_part;
+  const int32_t* phase;
+  const double* theta;        // [K, P]
+  const double* center;       // [q] or null
+  const double* scale;
+  double* slab_H;             // same partial slab layout as PassArgs
+  double* slab_g;
+  double* slab_ll;
+  int32_t q, F, P, intercept, NT, want_phase;
+  int32_t hist_doubles;       // LDS histogram doubles
+  int32_t nlev[kCatMaxFactors];    // dummy columns of factor f (L_f - 1)
+  int32_t doff[kCatMaxFactors];    // parameter index of factor f's first dummy
+  int32_t nd_off[kCatMaxFactors];  // LDS: [rep][nlev][q + 1] (w, w x_0 ..)
+  int32_t nd_rep[kCatMaxFactors];  // replicas (power of two)
+  int32_t g_off[kCatMaxFactors];   // LDS: [rep][nlev] gradient
+  int32_t pr_off[kCatMaxPairs];    // LDS: pair (f < g) [rep][nlev_f][nlev_g]
+  int32_t pr_rep[kCatMaxPairs];
+};
+
 // Launchers (defined in the .hip files).
+hipError_t launch_cat_pass(const CatArgs& a, bool standardize, int n_chunks, hipStream_t s);
+size_t cat_lds_bytes(const CatArgs& a);  // dynamic LDS of the pass
+constexpr int kCatStaticLds = 4 * (5 * kCatMaxFactors + 2 * kCatMaxPairs);  // its tables
+hipError_t launch_cat_presence(const CatArgs& a, int n_chunks, int32_t* counts, int32_t* bad,
+                               hipStream_t s);
+hipError_t launch_cat_mark(const CatArgs& a, const int32_t* pcb, const int32_t* counts,
+                           const int32_t* bad, int K, int32_t* phase, int32_t* status,
+                           int32_t* bad_part, hipStream_t s);
 hipError_t launch_wide_row(const WideArgs& a, bool standardize, int family, int n_chunks,
                            hipStream_t s);
 hipError_t launch_wide_gram(const WideArgs& a, bool standardize, bool f64, hipStream_t s);

@@ -114,38 +114,116 @@ AIRLINE_NUMERIC = 9
 AIRLINE_FACTORS = (12, 7, 20, 69, 69)  # Month, DayOfWeek, UniqueCarrier, Origin, Dest
 
 
-def simulate_dummy_design(n, seed=2019, numeric=AIRLINE_NUMERIC, factors=AIRLINE_FACTORS,
-                          device=None):
-    """Synthetic airline-like logistic data (BASELINE config 3), generated with
-    torch ops on ``device`` ("cpu" allowed: test and baseline plumbing).
+def simulate_categorical(n, seed=2019, numeric=AIRLINE_NUMERIC, factors=AIRLINE_FACTORS,
+                         device=None):
+    """Synthetic airline-like logistic data (BASELINE config 3) in the
+    categorical-code layout, generated with torch ops on ``device`` ("cpu"
+    allowed: test and baseline plumbing).
 
-    Columns: ``numeric`` U(-1/2, 1/2) features, then for each factor with L
-    levels the L-1 dummy columns of levels 1..L-1 (level 0 is the baseline);
-    codes are skewed towards low levels (code = floor(L u^2)) like airport and
-    carrier frequencies.  y ~ Bernoulli(sigmoid(-0.3 + X beta*)) with
-    beta*_numeric ~ U(-1, 1) and dummy effects ~ 0.3 N(0, 1) (fixed by
-    ``seed``; the rows by ``seed`` too).  Returns (X [n, p] fp64, y [n] fp64);
-    fit it with ``fit_intercept=True``."""
+    ``numeric`` U(-1/2, 1/2) columns and, per factor with L levels, a uint8 code
+    skewed towards low levels (code = floor(L u^2), like airport and carrier
+    frequencies; code 0 is the baseline level).  y ~ Bernoulli(sigmoid(-0.3 +
+    x beta*_num + sum_f beta*_f[code_f])) with beta*_num ~ U(-1, 1) and dummy
+    effects ~ 0.3 N(0, 1) (fixed by ``seed``; the rows by ``seed`` too).
+    Returns (Xn [n, numeric] fp64, codes [n, F] uint8, y [n] fp64, levels
+    [F] int32 numpy); fit with ``fit_intercept=True``."""
     dev = torch.device(device) if device is not None else torch.device("cuda")
     n = int(n)
-    p = numeric + sum(L - 1 for L in factors)
+    D = sum(L - 1 for L in factors)
     gb = torch.Generator(device="cpu").manual_seed(int(seed) ^ 0x5EED)
     beta = torch.cat([torch.rand(numeric, generator=gb, dtype=torch.float64) * 2 - 1,
-                      0.3 * torch.randn(p - numeric, generator=gb, dtype=torch.float64)])
+                      0.3 * torch.randn(D, generator=gb, dtype=torch.float64)]).to(dev)
     g = torch.Generator(device=dev).manual_seed(int(seed))
-    X = torch.zeros((n, p), dtype=torch.float64, device=dev)
-    X[:, :numeric] = torch.rand((n, numeric), generator=g, dtype=torch.float64, device=dev) - 0.5
-    rows = torch.arange(n, device=dev)
+    Xn = torch.rand((n, numeric), generator=g, dtype=torch.float64, device=dev) - 0.5
+    codes = torch.empty((n, len(factors)), dtype=torch.uint8, device=dev)
+    eta = Xn @ beta[:numeric] - 0.3
     col = numeric
-    for L in factors:
+    for f, L in enumerate(factors):
         u = torch.rand((n,), generator=g, dtype=torch.float64, device=dev)
         code = torch.clamp((L * u * u).long(), max=L - 1)
-        m = code > 0
-        X[rows[m], col + code[m] - 1] = 1.0
+        codes[:, f] = code.to(torch.uint8)
+        eff = torch.cat([torch.zeros(1, dtype=torch.float64, device=dev), beta[col:col + L - 1]])
+        eta = eta + eff[code]
         col += L - 1
-    eta = X @ beta.to(dev) - 0.3
     y = (torch.rand((n,), generator=g, dtype=torch.float64, device=dev) < torch.sigmoid(eta)).double()
-    return X, y
+    return Xn, codes, y, np.asarray(factors, dtype=np.int32)
+
+
+def expand_categorical(Xn, codes, levels):
+    """Dense dummy design [n, q + sum(L_f - 1)] of a categorical-code layout
+    (the columns pd.get_dummies + the baseline drop of models.py:62-69 give).
+    Works on torch tensors (any device) -- the dense baseline layout, not the
+    product path."""
+    n, q = Xn.shape
+    levels = [int(L) for L in levels]
+    X = torch.zeros((n, q + sum(L - 1 for L in levels)), dtype=torch.float64, device=Xn.device)
+    X[:, :q] = Xn
+    rows = torch.arange(n, device=Xn.device)
+    col = q
+    for f, L in enumerate(levels):
+        c = codes[:, f].long()
+        m = c > 0
+        X[rows[m], col + c[m] - 1] = 1.0
+        col += L - 1
+    return X
+
+
+def simulate_dummy_design(n, seed=2019, numeric=AIRLINE_NUMERIC, factors=AIRLINE_FACTORS,
+                          device=None):
+    """The same data as ``simulate_categorical`` as a dense dummy-coded design
+    (the reference's layout after models.py:56-91).  Returns (X [n, p] fp64,
+    y [n] fp64); fit it with ``fit_intercept=True``."""
+    Xn, codes, y, levels = simulate_categorical(n, seed, numeric, factors, device)
+    return expand_categorical(Xn, codes, levels), y
+
+
+def encode_categorical(sample_df, Y_name, dummy_info, dummy_factors_baseline=()):
+    """Categorical-code layout of one data chunk with the reference's dummy
+    semantics (dlsa/models.py:56-91): dropped levels -> "000_OTHERS"
+    (models.py:59), one column per sorted selected dummy name except the
+    baselines (models.py:66-79), numeric columns sorted by name (models.py:70).
+
+    Returns a dict: ``Xn`` [n, q] fp64, ``codes`` [n, F] uint8 (0 = baseline),
+    ``levels`` [F] int32 (= dummy columns + 1), ``numeric`` / ``cols`` (the
+    reference's column names, intercept excluded), ``unknown`` (a value outside
+    the selected and baseline names: the reference's column-set check fails,
+    models.py:84) and ``counts`` (rows per dummy column)."""
+    factors = list(dummy_info["factor_selected"].keys())
+    dropped = {k: v for k, v in dummy_info["factor_dropped"].items() if len(v) > 0}
+    df = sample_df.replace(dropped, "000_OTHERS") if dropped else sample_df
+    numeric = sorted(set(df.columns.drop(["partition_id", Y_name])) - set(factors))
+    base = set(dummy_factors_baseline)
+    n = len(df)
+    codes = np.zeros((n, len(factors)), dtype=np.uint8)
+    levels = np.zeros(len(factors), dtype=np.int32)
+    cols = list(numeric)
+    unknown = False
+    counts = []
+    for fi, f in enumerate(factors):
+        names = [c for c in sorted(dummy_info["factor_selected_names"][f]) if c not in base]
+        if len(names) > 255:
+            raise ValueError(f"factor {f}: {len(names)} dummy columns > 255 (uint8 codes)")
+        lut = {nm: j + 1 for j, nm in enumerate(names)}
+        for b in base:
+            if b.startswith(f + "_"):
+                lut.setdefault(b, 0)
+        vals = df[f].to_numpy()
+        uniq, inv = np.unique(np.asarray([f"{f}_{v}" for v in vals], dtype=object).astype(str),
+                              return_inverse=True)
+        mapped = np.array([lut.get(u, -1) for u in uniq], dtype=np.int64)
+        c = mapped[inv] if n else np.zeros(0, dtype=np.int64)
+        if (c < 0).any():
+            unknown = True
+            c = np.where(c < 0, 0, c)
+        codes[:, fi] = c
+        levels[fi] = len(names) + 1
+        counts.append(np.bincount(c, minlength=len(names) + 1)[1:])
+        cols.extend(names)
+    Xn = np.ascontiguousarray(df[numeric].to_numpy(dtype=np.float64)) if numeric else \
+        np.zeros((n, 0), dtype=np.float64)
+    return {"Xn": Xn, "codes": codes, "levels": levels, "numeric": numeric, "cols": cols,
+            "unknown": unknown,
+            "counts": np.concatenate(counts) if counts else np.zeros(0, dtype=np.int64)}
 
 
 def partition_offsets(partition_id, num_partitions=None):
@@ -269,6 +347,69 @@ def logistic_model_batched(X, y, offsets, fit_intercept=False, center=None, scal
     return BatchedFit(theta, sig, sigt, ll, iters, status, offs, bool(fit_intercept), stats)
 
 
+def logistic_model_batched_categorical(Xn, codes, y, offsets, levels, fit_intercept=False,
+                                       center=None, scale=None, max_iter=100, tol=1e-10,
+                                       record_timing=False, rows_per_chunk=0, warm_start=True,
+                                       device=None):
+    """Batched local logistic fit on the categorical-code layout (the dummy
+    branch of dlsa/models.py:56-91, BASELINE config 3) without materialising
+    the dummy matrix: the one-hot blocks of X^T W X are LDS histograms in the
+    HIP pass (``dlsa_logistic_fit_categorical``).
+
+    Xn: [n, q] fp64 numeric columns; codes: [n, F] uint8 level codes (0 =
+    baseline, c = dummy column c of the factor); levels: F ints (dummy columns
+    + 1); ``center``/``scale`` [q] standardise the numeric columns only
+    (models.py:99-101).  Parameters: [intercept] [numeric] [factor 0 dummies]
+    ...  A partition with a dummy column that has no rows gets status
+    "missing_level" and all-zero outputs (the reference's zero frame)."""
+    dev = _require_gpu(device)
+    Xd = _dev_f64(Xn, dev)
+    if Xd.dim() != 2:
+        raise ValueError("Xn must be 2-D [n, q]")
+    n, q = Xd.shape
+    if isinstance(codes, torch.Tensor):
+        cd8 = codes.to(device=dev, dtype=torch.uint8).contiguous()
+    else:
+        cd8 = torch.from_numpy(np.ascontiguousarray(np.asarray(codes, dtype=np.uint8))).to(dev)
+    if cd8.dim() != 2 or cd8.shape[0] != n:
+        raise ValueError("codes must be [n, F]")
+    F = cd8.shape[1]
+    lv = np.ascontiguousarray(np.asarray(levels, dtype=np.int32).reshape(-1))
+    if lv.size != F:
+        raise ValueError("levels must have F entries")
+    yd = _dev_f64(y, dev).reshape(-1)
+    offs = np.ascontiguousarray(np.asarray(offsets, dtype=np.int64))
+    K = offs.size - 1
+    if K < 1 or offs[0] != 0 or offs[-1] != n or np.any(np.diff(offs) < 0) or yd.numel() != n:
+        raise ValueError("offsets must be non-decreasing, start at 0 and end at n; y has n rows")
+    P = int(bool(fit_intercept)) + q + int((lv - 1).sum())
+    cen = sca = None
+    if center is not None or scale is not None:
+        cen = _dev_f64(center, dev).reshape(-1)
+        sca = _dev_f64(scale, dev).reshape(-1)
+        if cen.numel() != q or sca.numel() != q:
+            raise ValueError("center/scale must have q entries (numeric columns)")
+    theta = torch.empty((K, P), dtype=torch.float64, device=dev)
+    sig = torch.empty((K, P, P), dtype=torch.float64, device=dev)
+    sigt = torch.empty((K, P), dtype=torch.float64, device=dev)
+    ll = torch.empty((K,), dtype=torch.float64, device=dev)
+    iters = torch.empty((K,), dtype=torch.int32, device=dev)
+    status = torch.empty((K,), dtype=torch.int32, device=dev)
+    lib = _hip.load()
+    opt = _hip.default_options()
+    opt.record_timing = 1 if record_timing else 0
+    opt.rows_per_chunk = int(rows_per_chunk)
+    opt.warm_start = 1 if warm_start else 0
+    rc = lib.dlsa_logistic_fit_categorical(
+        _ptr(Xd), _ptr(cd8), _ptr(yd), offs.ctypes.data_as(ctypes.c_void_p), K, q, F,
+        lv.ctypes.data_as(ctypes.c_void_p), int(bool(fit_intercept)), _ptr(cen), _ptr(sca),
+        int(max_iter), float(tol), _ptr(theta), _ptr(sig), _ptr(sigt), _ptr(ll), _ptr(iters),
+        _ptr(status), ctypes.byref(opt), _stream(dev))
+    _hip.check(rc, "dlsa_logistic_fit_categorical")
+    return BatchedFit(theta, sig, sigt, ll, iters, status, offs, bool(fit_intercept),
+                      _hip.last_fit_stats())
+
+
 def ols_model_batched(X, y, offsets, fit_intercept=False, center=None, scale=None,
                       rows_per_chunk=0, record_timing=False, device=None):
     """Batched local OLS (linear DLSA path): per
@@ -377,6 +518,46 @@ def _design(sample_df, Y_name, dummy_info, dummy_factors_baseline):
     return x_train, list(x_train.columns), list(x_train.columns), False
 
 
+def _logistic_model_codes(sample_df, Y_name, fit_intercept, dummy_info, dummy_factors_baseline,
+                          data_info):
+    """Dummy branch of logistic_model on the categorical-code layout (no dense
+    dummy matrix).  None when the design exceeds the kernel's limits (F <= 16
+    factors, intercept + numeric <= 16, P <= 192): the caller then builds the
+    dense design."""
+    import pandas as pd
+
+    icpt = ["intercept"] if fit_intercept else []
+    enc = encode_categorical(sample_df, Y_name, dummy_info, dummy_factors_baseline)
+    q, F = enc["Xn"].shape[1], enc["codes"].shape[1]
+    P = len(icpt) + len(enc["cols"])
+    if F > 16 or len(icpt) + q > 16 or P > _hip.MAX_P_FUSED:
+        return None
+    cols = enc["cols"]
+    if enc["unknown"] or (enc["counts"] == 0).any():
+        absent = [c for c, m in zip(cols[q:], enc["counts"]) if m == 0]
+        warnings.warn("Dummies:" + str(set(absent)) + "missing in this data chunk "
+                      + str((len(sample_df), len(cols))) + "Skip modeling this part of data.")
+        return pd.DataFrame(0, index=np.arange(P),
+                            columns=["par_id", "coef", "Sig_invMcoef"] + icpt + cols)
+    center = scale = None
+    if len(data_info) > 0 and q > 0:
+        center = np.array([_describe_row(data_info, c, 1) for c in enc["numeric"]])
+        scale = np.array([_describe_row(data_info, c, 2) for c in enc["numeric"]])
+    y = np.asarray(sample_df[Y_name], dtype=np.float64)
+    fit = logistic_model_batched_categorical(enc["Xn"], enc["codes"], y, np.array([0, y.size]),
+                                             enc["levels"], fit_intercept=fit_intercept,
+                                             center=center, scale=scale)
+    coef = fit.theta[0].cpu().numpy()
+    sig = fit.sig_inv[0].cpu().numpy()
+    sigt = fit.sig_inv_theta[0].cpu().numpy()
+    out = pd.DataFrame(np.column_stack([coef, sigt, sig]),
+                       columns=pd.Index(["coef", "Sig_invMcoef"] + icpt + cols))
+    out.insert(0, "par_id", np.arange(P))
+    if out.isna().values.any():
+        warnings.warn("NAs appear in the final output")
+    return out
+
+
 def logistic_model(sample_df, Y_name, fit_intercept=False, dummy_info=[], dummy_factors_baseline=[],
                    data_info=[]):
     """Run the logistic model on one partition (dlsa/models.py:42-147).
@@ -390,6 +571,11 @@ def logistic_model(sample_df, Y_name, fit_intercept=False, dummy_info=[], dummy_
     import pandas as pd
 
     icpt = ["intercept"] if fit_intercept else []
+    if len(dummy_info) > 0:
+        out = _logistic_model_codes(sample_df, Y_name, fit_intercept, dummy_info,
+                                    dummy_factors_baseline, data_info)
+        if out is not None:
+            return out
     x_train, numeric, cols, missing = _design(sample_df, Y_name, dummy_info, dummy_factors_baseline)
     if missing:
         warnings.warn("Dummies:" + str(set(cols) - set(x_train.columns))

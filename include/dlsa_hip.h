@@ -55,6 +55,9 @@ extern "C" {
 #define DLSA_STATUS_SINGULAR 2    /* X^T W X not positive definite */
 #define DLSA_STATUS_EMPTY 3       /* no rows: zero block, like models.py:84-91 */
 #define DLSA_STATUS_NONFINITE 4   /* NaN/Inf in the data or the iterates */
+#define DLSA_STATUS_MISSING_LEVEL 5  /* categorical fit: a selected dummy level has no
+                                        rows in the partition -> the reference's
+                                        all-zero frame (models.py:84-91) */
 
 /* Hessian arithmetic of the Newton passes.  The gradient, eta, the weights
  * and the returned log-likelihood and Sig_inv are fp64 in every mode; the
@@ -185,6 +188,36 @@ int dlsa_logistic_loglik_batched(const double* X, const double* y,
                                  int32_t fit_intercept, const double* center,
                                  const double* scale, const double* betas,
                                  int32_t n_beta, double* loglik, void* stream);
+
+/*
+ * Batched local logistic fit on a categorical-code layout -- the dummy branch
+ * of dlsa/models.py:56-91 logistic_model() (airline design, BASELINE config
+ * 3) without materialising the dummy matrix.  Row i of partition k holds
+ *   Xn[i, 0:q]     q numeric columns (fp64, standardised by center/scale
+ *                  [q] like models.py:99-101 -- dummies are never standardised)
+ *   codes[i, 0:F]  one uint8 level code per factor f: 0 = the baseline level
+ *                  (dropped, models.py:67/77), c in 1..levels[f]-1 = dummy
+ *                  column c of factor f
+ *   y[i]           0/1 label.
+ * Parameters (P = fit_intercept + q + sum_f (levels[f] - 1) <= DLSA_MAX_P_FUSED):
+ *   [intercept] [numeric 0..q-1] [factor 0 dummies 1..L0-1] [factor 1 ...] ...
+ * The one-hot blocks of X^T W X are computed as weighted histograms in LDS
+ * (exact fp64); outputs are as in dlsa_logistic_fit_batched (theta,
+ * Sig_inv = X^T W X of the dummy-expanded design at theta, ...).  A partition
+ * in which some dummy column has no rows gets DLSA_STATUS_MISSING_LEVEL and
+ * all-zero outputs, the reference's "fake zero matrix".  Codes >= levels[f]
+ * fail the call with DLSA_E_INVALID.  Limits: F <= 16, levels[f] in 1..256,
+ * fit_intercept + q <= 16.  levels is a HOST array [F]; opt may be NULL
+ * (hessian_mode is ignored: every pass is exact fp64).
+ */
+int dlsa_logistic_fit_categorical(const double* Xn, const uint8_t* codes, const double* y,
+                                  const int64_t* offsets, int32_t K, int32_t q, int32_t F,
+                                  const int32_t* levels, int32_t fit_intercept,
+                                  const double* center, const double* scale,
+                                  int32_t max_iter, double tol, double* theta,
+                                  double* sig_inv, double* sig_inv_theta, double* loglik,
+                                  int32_t* iters, int32_t* status,
+                                  const dlsa_fit_options* opt, void* stream);
 
 /* Timing/iteration record of the calling thread's last fit. */
 int dlsa_last_fit_stats(dlsa_fit_stats* out);

@@ -17,6 +17,8 @@ the agreement).  See DESIGN.md section "Oracle".
 """
 
 from .dlsa_oracle import (  # noqa: F401
+    dummy_design,
+    expand_codes,
     simulate_logistic_arrays,
     simulate_logistic,
     simulate_counter,

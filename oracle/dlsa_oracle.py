@@ -200,6 +200,58 @@ def logistic_fit_partitions(X, y, offsets, **kw):
             np.array([o["iters"] for o in outs]))
 
 
+def dummy_design(numeric, factors, dummy_info, dummy_factors_baseline=()):
+    """Dense design of one data chunk in the reference's dummy branch,
+    dlsa/models.py:56-91, restated without pandas:
+    dropped levels -> "000_OTHERS" (:59); a dummy per level (:62-65) named
+    "<factor>_<value>", baselines dropped (:67, :77); columns = sorted numeric
+    names (:70) then each factor's sorted selected names (:72-75).  Returns
+    (X [n, p], column names, missing) where ``missing`` is the reference's
+    column-set check (:84): the chunk lacks a selected column or has a value
+    outside the selected names -> the caller returns the all-zero frame.
+
+    numeric: {name: [n] array}; factors: {name: [n] values} (any order)."""
+    base = set(dummy_factors_baseline)
+    names_num = sorted(numeric)
+    cols = list(names_num)
+    blocks = [np.column_stack([np.asarray(numeric[c], dtype=np.float64) for c in names_num])] \
+        if names_num else []
+    n = len(next(iter(numeric.values()))) if numeric else len(next(iter(factors.values())))
+    present = set(names_num)
+    for f in dummy_info["factor_selected"]:
+        dropped = set(str(v) for v in dummy_info["factor_dropped"].get(f, []))
+        vals = ["000_OTHERS" if str(v) in dropped else str(v) for v in factors[f]]
+        names = [f"{f}_{v}" for v in vals]
+        present |= set(names) - base
+        sel = [c for c in sorted(dummy_info["factor_selected_names"][f]) if c not in base]
+        cols.extend(sel)
+        idx = {c: j for j, c in enumerate(sel)}
+        B = np.zeros((n, len(sel)))
+        for i, nm in enumerate(names):
+            j = idx.get(nm)
+            if j is not None:
+                B[i, j] = 1.0
+        blocks.append(B)
+    X = np.hstack(blocks) if blocks else np.zeros((n, 0))
+    return X, cols, present != set(cols)
+
+
+def expand_codes(Xn, codes, levels):
+    """Dense dummy design of a categorical-code layout: numeric columns, then
+    per factor f the levels[f] - 1 indicator columns of codes 1..L-1 (code 0
+    = the dropped baseline level)."""
+    Xn = np.asarray(Xn, dtype=np.float64)
+    codes = np.asarray(codes)
+    blocks = [Xn]
+    for f, L in enumerate(levels):
+        B = np.zeros((Xn.shape[0], int(L) - 1))
+        c = codes[:, f].astype(np.int64)
+        m = c > 0
+        B[np.nonzero(m)[0], c[m] - 1] = 1.0
+        blocks.append(B)
+    return np.hstack(blocks)
+
+
 def logistic_loglik(X, y, betas, fit_intercept=False, center=None, scale=None):
     """Restates the likelihood loop of ``logistic_model_eval``
     (dlsa/models.py:196-225): for each candidate column beta,

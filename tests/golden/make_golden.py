@@ -263,5 +263,81 @@ def main():
     print("standardized done")
 
 
+def golden_dummy():
+    """G. The dummy branch of logistic_model (models.py:56-91): string and int
+    factors, dropped levels -> 000_OTHERS, baseline dummies dropped, data_info
+    standardisation of the numeric columns, intercept; partition 4 lacks a
+    selected level -> the reference's all-zero frame."""
+    import json
+    import tempfile
+
+    import dlsa.dummies as RD  # reference
+
+    rs = np.random.RandomState(11)
+    n = 8000
+    carriers = np.array(["AA", "DL", "UA", "WN", "B6", "NK", "F9"])
+    origins = np.array(["ATL", "ORD", "DFW", "DEN", "LAX", "SEA", "SFO", "BOS"])
+    month = rs.randint(1, 7, size=n)
+    carrier = carriers[np.minimum((7 * rs.rand(n) ** 2).astype(int), 6)]
+    origin = origins[np.minimum((8 * rs.rand(n) ** 1.5).astype(int), 7)]
+    dist = rs.exponential(800.0, size=n) + 100.0
+    dep = rs.uniform(0, 24, size=n)
+    pid = np.arange(n) % 4
+    # partition 4: 400 rows, never SEA (a selected Origin level); it keeps the
+    # baseline (000_OTHERS) levels: the reference raises KeyError on a chunk
+    # without a baseline level (models.py:67 drops them unconditionally)
+    m4 = 400
+    month = np.concatenate([month, rs.randint(1, 7, size=m4)])
+    carrier = np.concatenate([carrier, carriers[rs.randint(0, 7, size=m4)]])
+    origin = np.concatenate([origin, np.array(["ATL", "ORD", "DFW", "BOS", "SFO"])[
+        rs.randint(0, 5, size=m4)]])
+    dist = np.concatenate([dist, rs.exponential(800.0, size=m4) + 100.0])
+    dep = np.concatenate([dep, rs.uniform(0, 24, size=m4)])
+    pid = np.concatenate([pid, np.full(m4, 4)])
+    eff_c = dict(zip(carriers, [0.0, 0.3, -0.2, 0.5, -0.4, 0.2, 0.1]))
+    eff_o = dict(zip(origins, [0.0, 0.2, -0.3, 0.4, 0.1, -0.2, 0.3, -0.1]))
+    eta = (-0.2 + 0.4 * (dist - 900) / 800 - 0.05 * (dep - 12) + 0.1 * (month - 3.5)
+           + np.array([eff_c[c] for c in carrier]) + np.array([eff_o[o] for o in origin]))
+    label = (rs.rand(n + m4) < 1 / (1 + np.exp(-eta))).astype(float)
+    df = pd.DataFrame({"partition_id": pid.astype(float), "label": label, "Month": month,
+                       "UniqueCarrier": carrier, "Origin": origin, "Distance": dist,
+                       "DepTime": dep})
+    factors = ["Month", "UniqueCarrier", "Origin"]
+    counts = RD.dummy_factors_counts(df, factors)
+    with tempfile.TemporaryDirectory() as tmp:
+        info_d = RD.select_dummy_factors(counts, keep_top=[1, 0.8, 0.9],
+                                         replace_with="000_OTHERS",
+                                         pickle_file=os.path.join(tmp, "dummy_info.pkl"))
+    info_d = {k: {f: [x.item() if hasattr(x, "item") else x for x in v] for f, v in d.items()}
+              for k, d in info_d.items()}
+    baseline = ["Month_1", "UniqueCarrier_000_OTHERS", "Origin_000_OTHERS"]
+    numeric = ["DepTime", "Distance"]
+    info = pd.DataFrame({"summary": ["count", "mean", "stddev", "min", "max"]})
+    for c in numeric:
+        v = df[c].to_numpy()
+        info[c] = [str(v.size), repr(float(v.mean())), repr(float(v.std(ddof=1))),
+                   repr(float(v.min())), repr(float(v.max()))]
+    _TOL[0] = 1e-12
+    outs, cols = [], None
+    for _, g in df.groupby("partition_id", sort=True):
+        g = g.reset_index(drop=True)
+        o = RM.logistic_model(g, "label", fit_intercept=True, dummy_info=info_d,
+                              dummy_factors_baseline=baseline, data_info=info)
+        outs.append(o.to_numpy(dtype=np.float64))
+        cols = list(o.columns) if cols is None else cols
+    np.savez_compressed(
+        os.path.join(OUT, "dummy_branch.npz"), pid=pid, label=label, month=month,
+        carrier=carrier.astype("U8"), origin=origin.astype("U8"), distance=dist, deptime=dep,
+        dummy_info=json.dumps(info_d), baseline=np.array(baseline, dtype="U32"),
+        info=info.to_numpy().astype("U40"), info_cols=np.array(list(info.columns), dtype="U32"),
+        outs=np.stack(outs), cols=np.array(cols, dtype="U40"))
+    print("dummy branch done:", np.stack(outs).shape, "zero frame:",
+          not np.abs(outs[4]).any())
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "dummy":
+        golden_dummy()
+    else:
+        main()
+        golden_dummy()

@@ -237,3 +237,40 @@ def test_wlse_cholesky_matches_lstsq_and_falls_back():
     v[7] = 0.0
     ref = np.linalg.lstsq(S, v, rcond=None)[0]
     assert np.allclose(wlse(S, v), ref, rtol=1e-10, atol=1e-12)
+
+
+def test_encode_categorical_matches_reference_design(golden_dir):
+    """The product's categorical-code encoding (dlsa_amd.models.encode_categorical)
+    expands to exactly the oracle's restatement of the reference dummy design
+    (models.py:56-91) and the reference's column names; the missing-level
+    partition is detected from the level counts."""
+    from test_oracle_golden import _dummy_fixture
+
+    from dlsa_amd.models import encode_categorical
+
+    g, df, dinfo, base, info = _dummy_fixture(golden_dir)
+    cols = [str(c) for c in g["cols"]][4:]
+    for k in range(5):
+        part = df[df["partition_id"] == k].reset_index(drop=True)
+        enc = encode_categorical(part, "label", dinfo, base)
+        assert enc["cols"] == cols and enc["numeric"] == ["DepTime", "Distance"]
+        assert enc["codes"].dtype == np.uint8 and enc["levels"].tolist() == [6, 5, 7]
+        num = {c: part[c].to_numpy() for c in ("Distance", "DepTime")}
+        fac = {c: part[c].to_numpy() for c in ("Month", "UniqueCarrier", "Origin")}
+        X, _, missing = O.dummy_design(num, fac, dinfo, base)
+        assert np.array_equal(O.expand_codes(enc["Xn"], enc["codes"], enc["levels"]), X)
+        assert missing == (bool((enc["counts"] == 0).any()) or enc["unknown"])
+        assert missing == (k == 4)
+
+
+def test_categorical_generator_expands_to_dummy_design():
+    """Config-3 data: the categorical-code generator and the dense design are
+    the same draws (expand(codes) == simulate_dummy_design)."""
+    torch = pytest.importorskip("torch")
+    from dlsa_amd.models import simulate_categorical, simulate_dummy_design
+
+    Xn, codes, y, levels = simulate_categorical(5000, seed=9, device="cpu")
+    X, y2 = simulate_dummy_design(5000, seed=9, device="cpu")
+    assert codes.dtype == torch.uint8 and codes.shape == (5000, 5)
+    assert np.array_equal(O.expand_codes(Xn.numpy(), codes.numpy(), levels), X.numpy())
+    assert torch.equal(y, y2)

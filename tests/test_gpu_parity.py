@@ -428,3 +428,120 @@ def test_config5_shape_sampled_partitions(torch_cuda, M):
     sel = dlsa(comb.iloc[:, 2:], comb["beta_byOLS"], K * nk)
     sup = set(np.nonzero(sel["beta_byBIC"].to_numpy())[0].tolist())
     assert set(range(200)) <= sup  # the 0.4 p true nonzeros are all kept
+
+
+# ---------------------------------------------------------------------------
+# categorical-code layout (dummy branch, BASELINE config 3)
+# ---------------------------------------------------------------------------
+
+
+def test_logistic_model_dummy_branch_vs_reference(golden_dir, torch_cuda, M):
+    """The reference-signature logistic_model with dummy_info / baseline /
+    data_info (models.py:42-147) runs the categorical-code HIP pass and
+    reproduces the reference's frames; the partition missing a selected level
+    returns the all-zero frame with the reference's warning."""
+    from test_oracle_golden import _dummy_fixture
+
+    g, df, dinfo, base, info = _dummy_fixture(golden_dir)
+    outs = g["outs"]
+    for k in range(outs.shape[0]):
+        part = df[df["partition_id"] == k].reset_index(drop=True)
+        if k == 4:
+            with pytest.warns(UserWarning, match="missing in this data chunk"):
+                o = M.logistic_model(part, "label", True, dinfo, base, info)
+            assert list(o.columns) == [str(c) for c in g["cols"]]
+            assert not np.abs(o.to_numpy(dtype=np.float64)).any()
+            continue
+        o = M.logistic_model(part, "label", True, dinfo, base, info)
+        assert list(o.columns) == [str(c) for c in g["cols"]]
+        got, ref = o.to_numpy(dtype=np.float64), outs[k]
+        assert _rel(got[:, 1], ref[:, 1]) < REL
+        assert _rel(got[:, 3:], ref[:, 3:]) < REL
+        assert _rel(got[:, 2], ref[:, 2]) < REL
+
+
+def _cat_case(q, levels, n_parts, seed, center=False):
+    rs = np.random.RandomState(seed)
+    sizes = [int(s) for s in rs.randint(3000, 9000, size=n_parts)]
+    n = sum(sizes)
+    Xn = rs.randn(n, q) * 2.0 + 1.0 if center else rs.rand(n, q) - 0.5
+    codes = np.stack([np.minimum((L * rs.rand(n) ** 2).astype(np.int64), L - 1)
+                      for L in levels], 1).astype(np.uint8) if levels else \
+        np.zeros((n, 0), np.uint8)
+    D = sum(L - 1 for L in levels)
+    beta = np.concatenate([rs.uniform(-1, 1, q) * (0.5 if center else 1.0), 0.4 * rs.randn(D)])
+    Xs = (Xn - 1.0) / 2.0 if center else Xn
+    X = O.expand_codes(Xs, codes, levels)
+    y = (rs.rand(n) < 1 / (1 + np.exp(-(X @ beta - 0.2)))).astype(np.float64)
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    return Xn, codes, y, off
+
+
+@pytest.mark.parametrize("q,levels,fi,std,rpc", [
+    (3, [4, 3], False, False, 0),                 # QN 4 bucket, no intercept
+    (7, [5, 5, 9], True, True, 1500),             # QN 8, standardised, multi-chunk partitions
+    (9, [12, 7, 20, 30, 30], True, False, 0),     # QN 10 (airline-like numeric block)
+    (11, [3] * 10, True, False, 0),               # QN 12, F = 10 (16-factor kernel)
+    (15, [4, 6], True, True, 2000),               # QN 16, 256-thread kernel
+])
+def test_categorical_vs_oracle(torch_cuda, M, q, levels, fi, std, rpc):
+    """Categorical-code pass (LDS histograms for the one-hot blocks) against
+    the oracle on the dense dummy expansion: every kernel bucket, replicated
+    and unreplicated histograms, standardisation, ragged partitions."""
+    Xn, codes, y, off = _cat_case(q, levels, 3, seed=q, center=std)
+    c = np.full(q, 1.0) if std else None
+    s = np.full(q, 2.0) if std else None
+    fit = M.logistic_model_batched_categorical(Xn, codes, y, off, levels, fit_intercept=fi,
+                                               center=c, scale=s, rows_per_chunk=rpc)
+    D = sum(L - 1 for L in levels)
+    X = O.expand_codes(Xn, codes, levels)
+    kw = {}
+    if std:
+        kw = dict(center=np.concatenate([c, np.zeros(D)]), scale=np.concatenate([s, np.ones(D)]))
+    th, S, St, ll, it = O.logistic_fit_partitions(X, y, off, fit_intercept=fi, **kw)
+    assert (fit.status.cpu().numpy() == 0).all(), fit.status
+    assert fit.theta.shape == (3, int(fi) + q + D)
+    assert _rel(fit.theta.cpu(), th) < REL
+    assert _rel(fit.sig_inv.cpu(), S) < REL
+    assert _rel(fit.sig_inv_theta.cpu(), St) < REL
+    assert _rel(fit.loglik.cpu(), ll) < 1e-10
+
+
+def test_categorical_config3_geometry_vs_oracle_and_dense(torch_cuda, M):
+    """BASELINE config-3 shape (9 numeric + 5 factors -> P = 182) generated on
+    the device: categorical path vs the oracle and vs the dense mixed-Hessian
+    path on the expanded design; an empty partition (status empty) and a
+    partition missing a level (status missing_level, zero outputs)."""
+    torch = torch_cuda
+    Xn, codes, y, levels = M.simulate_categorical(4 * 20000 + 7, seed=7, device="cuda")
+    off = np.array([0, 20000, 40003, 40003, 60001, 80007], dtype=np.int64)
+    # partition 4: drop Dest level 5 (-> baseline) so that column has no rows
+    sl = slice(60001, 80007)
+    c4 = codes[sl, 4]
+    codes[sl, 4] = torch.where(c4 == 5, torch.zeros_like(c4), c4)
+    fit = M.logistic_model_batched_categorical(Xn, codes, y, off, levels, fit_intercept=True)
+    st = fit.status.cpu().numpy().tolist()
+    assert st == [0, 0, 3, 0, 5], st
+    X = O.expand_codes(Xn.cpu().numpy(), codes.cpu().numpy(), levels)
+    keep = [0, 1, 3]
+    yh = y.cpu().numpy()
+    ref = [O.logistic_fit(X[off[k]:off[k + 1]], yh[off[k]:off[k + 1]], fit_intercept=True)
+           for k in keep]
+    assert fit.theta.shape == (5, 182)
+    assert _rel(fit.theta.cpu()[keep], np.stack([r["coef"] for r in ref])) < REL
+    assert _rel(fit.sig_inv.cpu()[keep], np.stack([r["Sig_inv"] for r in ref])) < REL
+    assert _rel(fit.sig_inv_theta.cpu()[keep], np.stack([r["Sig_invMcoef"] for r in ref])) < REL
+    for k in (2, 4):
+        assert not fit.theta[k].abs().max().item() and not fit.sig_inv[k].abs().max().item()
+    dense = M.logistic_model_batched(torch.from_numpy(X).cuda(), y, off, fit_intercept=True)
+    assert _rel(fit.theta.cpu()[keep], dense.theta.cpu()[keep]) < REL
+    assert _rel(fit.sig_inv.cpu()[keep], dense.sig_inv.cpu()[keep]) < REL
+
+
+def test_categorical_invalid_code_fails_loudly(torch_cuda, M):
+    from dlsa_amd._hip import DlsaHipError
+
+    Xn, codes, y, off = _cat_case(2, [3, 4], 2, seed=1)
+    codes[17, 1] = 4  # levels[1] = 4 -> valid codes 0..3
+    with pytest.raises(DlsaHipError, match="level codes"):
+        M.logistic_model_batched_categorical(Xn, codes, y, off, [3, 4], fit_intercept=True)
