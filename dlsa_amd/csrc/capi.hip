@@ -1017,11 +1017,17 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
     return DLSA_E_UNSUPPORTED;
   }
 
-  // chunks: ~2 workgroups (512 threads, one per CU at this LDS size) per CU,
-  // sized from the rows each level streams
-  auto cat_rpc = [&](int64_t rows) {
+  // chunks: one workgroup per CU at this LDS size, so a launch should be
+  // whole rounds of 256 workgroups: ~512 chunks, split evenly per partition
+  // (a ceil-rounded n/512 gave 5 chunks per config-3 partition -> 640 chunks,
+  // 3 rounds of which the last is half empty)
+  auto cat_rpc = [&](double frac, int64_t min_rows) {
     if (opt.rows_per_chunk > 0) return (int)opt.rows_per_chunk;
-    return (int)std::max<int64_t>(2048, std::min<int64_t>(rows / 512, 1 << 20));
+    int64_t nmax = 0;
+    for (int k = 0; k < K; ++k)
+      nmax = std::max(nmax, rows_used(offsets[k + 1] - offsets[k], frac, min_rows));
+    const int64_t per = std::max<int64_t>(1, 512 / std::max(K, 1));
+    return (int)std::max<int64_t>(1024, std::min<int64_t>((nmax + per - 1) / per, 1 << 24));
   };
   std::vector<Plan> plans;
   if (opt.warm_start) {
@@ -1029,13 +1035,13 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
     for (double frac : {1.0 / 16.0, 1.0 / 4.0}) {
       Plan qn;
       const int64_t lr = level_rows(offsets, K, frac, min_rows);
-      make_plan(offsets, K, P - ic, ic, cat_rpc(lr), qn, frac, min_rows);
+      make_plan(offsets, K, P - ic, ic, cat_rpc(frac, min_rows), qn, frac, min_rows);
       if (lr <= n_total / 2 && qn.n_chunks > 0) plans.push_back(std::move(qn));
     }
   }
   {
     Plan full;
-    make_plan(offsets, K, P - ic, ic, cat_rpc(n_total), full);
+    make_plan(offsets, K, P - ic, ic, cat_rpc(1.0, 0), full);
     plans.push_back(std::move(full));
   }
   const Plan& pl = plans.back();
@@ -1359,6 +1365,75 @@ int dlsa_logistic_loglik_batched(const double* X, const double* y, const int64_t
     DLSA_HIP_TRY(launch_loglik_eval(ea, pl.n_chunks, stream));
   }
   DLSA_HIP_TRY(launch_loglik_reduce(d_partial, d_pcb, K, n_beta, loglik, stream));
+  DLSA_HIP_TRY(hipStreamSynchronize(stream));
+  return DLSA_OK;
+}
+
+int dlsa_partition_rows(const int32_t* part_id, int64_t n, int32_t K, int32_t n_arrays,
+                        const void* const* src, void* const* dst, const int64_t* row_bytes,
+                        int64_t* offsets, int64_t* order, void* stream_) {
+  g_last_error.clear();
+  hipStream_t stream = (hipStream_t)stream_;
+  if (K < 1 || K > kPartMaxK || n < 0 || n_arrays < 0 || n_arrays > kPartMaxArrays ||
+      !offsets || (n_arrays > 0 && (!src || !dst || !row_bytes))) {
+    set_error("dlsa_partition_rows: need 1 <= K <= " + std::to_string(kPartMaxK) +
+              ", 0 <= n_arrays <= " + std::to_string(kPartMaxArrays) +
+              ", host src/dst/row_bytes arrays and a host offsets[K+1]");
+    return DLSA_E_INVALID;
+  }
+  for (int a = 0; a < n_arrays; ++a)
+    if (row_bytes[a] < 1 || (n > 0 && (!src[a] || !dst[a]))) {
+      set_error("dlsa_partition_rows: array " + std::to_string(a) + " has no rows or pointers");
+      return DLSA_E_INVALID;
+    }
+  if (n == 0) {
+    for (int k = 0; k <= K; ++k) offsets[k] = 0;
+    return DLSA_OK;
+  }
+  if (!part_id) {
+    set_error("dlsa_partition_rows: null part_id");
+    return DLSA_E_INVALID;
+  }
+  // ~2048 blocks of input rows (block order = input order: stable)
+  const int64_t rpb = std::max<int64_t>(kPartSubRows, (n + 2047) / 2048);
+  const int nb = (int)((n + rpb - 1) / rpb);
+  const int64_t off_counts = 0;
+  const int64_t off_bad = align_up(4LL * nb * K, 256);
+  const int64_t off_tot = align_up(off_bad + 4LL * nb, 256);
+  const int64_t off_offs = align_up(off_tot + 8LL * K, 256);
+  const int64_t total = align_up(off_offs + 8LL * (K + 1), 256);
+  char* ws = nullptr;
+  DLSA_HIP_TRY(hipMallocAsync((void**)&ws, total, stream));
+  struct Free {
+    char* p;
+    hipStream_t s;
+    ~Free() {
+      if (p) (void)hipFreeAsync(p, s);
+    }
+  } freer{ws, stream};
+  int32_t* counts = (int32_t*)(ws + off_counts);
+  int32_t* bad = (int32_t*)(ws + off_bad);
+  int64_t* totals = (int64_t*)(ws + off_tot);
+  int64_t* offs_dev = (int64_t*)(ws + off_offs);
+  DLSA_HIP_TRY(launch_partition_rows(part_id, n, K, rpb, nb, counts, bad, totals, offs_dev,
+                                     stream));
+  std::vector<int32_t> h_bad(nb);
+  DLSA_HIP_TRY(hipMemcpyAsync(h_bad.data(), bad, 4LL * nb, hipMemcpyDeviceToHost, stream));
+  DLSA_HIP_TRY(hipMemcpyAsync(offsets, offs_dev, 8LL * (K + 1), hipMemcpyDeviceToHost, stream));
+  DLSA_HIP_TRY(hipStreamSynchronize(stream));
+  int64_t nbad = 0;
+  for (int b = 0; b < nb; ++b) nbad += h_bad[b];
+  if (nbad) {
+    set_error("dlsa_partition_rows: " + std::to_string(nbad) + " partition ids outside [0, K)");
+    return DLSA_E_INVALID;
+  }
+  for (int k = 0; k < K; ++k)
+    if (offsets[k + 1] - offsets[k] > INT32_MAX) {
+      set_error("dlsa_partition_rows: a partition has more than 2^31 - 1 rows");
+      return DLSA_E_UNSUPPORTED;
+    }
+  DLSA_HIP_TRY(launch_partition_scatter(part_id, n, K, rpb, nb, counts, offs_dev, src, dst,
+                                        row_bytes, n_arrays, order, stream));
   DLSA_HIP_TRY(hipStreamSynchronize(stream));
   return DLSA_OK;
 }

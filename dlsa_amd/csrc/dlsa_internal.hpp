@@ -151,6 +151,19 @@ struct CatArgs {
   int32_t pr_rep[kCatMaxPairs];
 };
 
+// Row repartitioning (partition_rows.hip): stable counting sort by partition id.
+constexpr int kPartMaxArrays = 4;
+constexpr int kPartMaxK = 16000;    // LDS histogram / cursors
+constexpr int kPartSubRows = 4096;  // rows ranked per scatter sub-block
+hipError_t launch_partition_rows(const int32_t* pid, int64_t n, int K, int64_t rows_per_block,
+                                 int nb, int32_t* counts, int32_t* bad, int64_t* totals,
+                                 int64_t* offsets_dev, hipStream_t s);
+hipError_t launch_partition_scatter(const int32_t* pid, int64_t n, int K, int64_t rows_per_block,
+                                    int nb, const int32_t* base, const int64_t* offsets_dev,
+                                    const void* const* src, void* const* dst,
+                                    const int64_t* row_bytes, int n_arrays, int64_t* order,
+                                    hipStream_t s);
+
 // Launchers (defined in the .hip files).
 hipError_t launch_cat_pass(const CatArgs& a, bool standardize, int n_chunks, hipStream_t s);
 size_t cat_lds_bytes(const CatArgs& a);  // dynamic LDS of the pass

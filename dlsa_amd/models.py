@@ -207,10 +207,10 @@ def encode_categorical(sample_df, Y_name, dummy_info, dummy_factors_baseline=())
         for b in base:
             if b.startswith(f + "_"):
                 lut.setdefault(b, 0)
-        vals = df[f].to_numpy()
-        uniq, inv = np.unique(np.asarray([f"{f}_{v}" for v in vals], dtype=object).astype(str),
-                              return_inverse=True)
-        mapped = np.array([lut.get(u, -1) for u in uniq], dtype=np.int64)
+        import pandas as pd
+
+        inv, uniq = pd.factorize(df[f], sort=False)  # one name per distinct value
+        mapped = np.array([lut.get(f"{f}_{u}", -1) for u in uniq], dtype=np.int64)
         c = mapped[inv] if n else np.zeros(0, dtype=np.int64)
         if (c < 0).any():
             unknown = True

@@ -237,6 +237,26 @@ int dlsa_reduce_partitions(const double* sig_inv, const double* sig_inv_theta,
                            double* out, void* stream);
 
 /*
+ * Row repartitioning in HBM -- replaces the Spark shuffle that groups rows by
+ * partition before the map stage: `repartition(K, "partition_id")` + the
+ * `groupby("partition_id").apply(udf)` of projects/logistic_dlsa.py:303-325,
+ * with ids from monotonically_increasing_id() % K (:243-245) or a column.
+ * A stable counting sort: rows of partition k land in output rows
+ * offsets[k] .. offsets[k+1]-1 in their input order.
+ *  part_id   [n] int32 device, every id in [0, K) (else DLSA_E_INVALID)
+ *  src, dst, row_bytes  HOST arrays of n_arrays (<= 4) entries: device
+ *            pointers of row-major arrays with row_bytes bytes per row (e.g.
+ *            X [n, p] fp64 -> 8p, y -> 8, uint8 codes [n, F] -> F); dst must
+ *            not overlap src
+ *  offsets   [K+1] int64 HOST out (the layout every fit entry point takes)
+ *  order     [n] int64 device out or NULL: input row of each output row
+ * 1 <= K <= 16000.  Synchronises the stream (offsets are read back).
+ */
+int dlsa_partition_rows(const int32_t* part_id, int64_t n, int32_t K, int32_t n_arrays,
+                        const void* const* src, void* const* dst, const int64_t* row_bytes,
+                        int64_t* offsets, int64_t* order, void* stream);
+
+/*
  * Synthetic logistic data in HBM (the input generator of SURVEY 8(d) for
  * configs too large for the host): X[i, j] = u(seed, row0 + i, j) - 0.5 with
  * u a counter-based (splitmix64) U[0,1) double; beta* = 1 on the first

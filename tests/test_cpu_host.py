@@ -274,3 +274,33 @@ def test_categorical_generator_expands_to_dummy_design():
     assert codes.dtype == torch.uint8 and codes.shape == (5000, 5)
     assert np.array_equal(O.expand_codes(Xn.numpy(), codes.numpy(), levels), X.numpy())
     assert torch.equal(y, y2)
+
+
+def test_read_table_select_dropna_binarise(tmp_path):
+    """Host half of the ingest (logistic_dlsa.py:226-239) against pandas."""
+    import pandas as pd
+
+    from dlsa_amd.ingest import read_table
+
+    rs = np.random.RandomState(1)
+    df = pd.DataFrame({"a": rs.randn(500), "b": rs.rand(500), "c": rs.rand(500),
+                       "y": rs.randint(-3, 4, 500).astype(float)})
+    df.loc[[3, 17, 400], "a"] = np.nan
+    df.loc[[5], "c"] = np.nan  # not selected: keeps the row
+    df.to_csv(tmp_path / "t.csv", index=False)
+    t = read_table(str(tmp_path / "t.csv"), "y", ["b", "a"])
+    ref = df[["b", "a", "y"]].dropna().reset_index(drop=True)
+    ref["y"] = (ref["y"] > 0).astype(float)
+    assert list(t.columns) == ["b", "a", "y"]
+    assert np.array_equal(t.to_numpy(), ref.to_numpy())
+
+
+def test_ingest_fails_loudly_without_gpu():
+    torch = pytest.importorskip("torch")
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from dlsa_amd._hip import DlsaHipError
+    from dlsa_amd.ingest import repartition
+
+    with pytest.raises(DlsaHipError):
+        repartition(torch.zeros(4, dtype=torch.int32), 2, torch.zeros((4, 2)))
