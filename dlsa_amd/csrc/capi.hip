@@ -48,11 +48,16 @@ static bool use_perwave_pass() {
 // Pass kernel of a precision phase: the register-streaming pass (one wave
 // per chunk, all tiles in registers; P <= 112) or the cooperative LDS pass.
 // DLSA_PASS_F64 / DLSA_PASS_LOWP = reg | coop override the default.
-static bool use_reg_pass(int NT, bool f64) {
+// Default: the register pass for the OLS (gaussian) fp64 pass -- measured at
+// config 4 (p = 64, NT = 4): 16.8 ms vs 22.4 ms cooperative, as every tile of
+// X^T X fits one wave's registers and there is no row-phase transcendental
+// work to overlap; the cooperative pass elsewhere (config 2 fp64: 33.1 vs
+// 38.9 ms reg).
+static bool use_reg_pass(int NT, bool f64, int family = FAMILY_LOGISTIC) {
   if (NT > kRegMaxNT || use_perwave_pass()) return false;
   const char* e = getenv(f64 ? "DLSA_PASS_F64" : "DLSA_PASS_LOWP");
   if (e) return strcmp(e, "reg") == 0;
-  return false;
+  return f64 && family == FAMILY_GAUSSIAN;
 }
 
 // fp64 passes: the wave-specialised kernel (P <= 128) unless
@@ -73,8 +78,14 @@ static bool use_lite_pass(int NT, int p, int prec) {
   return false;
 }
 
-static int auto_rows_per_chunk(int64_t n_total, int NT = 0) {
+static int auto_rows_per_chunk(int64_t n_total, int NT = 0, int family = FAMILY_LOGISTIC) {
   if (const char* e = getenv("DLSA_ROWS_PER_CHUNK")) return std::max(64, atoi(e));
+  if (NT > 0 && family == FAMILY_GAUSSIAN && use_reg_pass(NT, true, family)) {
+    // OLS register pass: ~16k one-wave chunks (config 4 sweep, ms per pass /
+    // per fit: 2080 chunks 21.6, 4224 18.5, 8320 16.7 / 17.8, 12.5k 16.1 / 17.4,
+    // 16.7k 15.7 / 16.9 -- the solve sums more chunk partials)
+    return (int)std::max<int64_t>(1024, std::min<int64_t>(n_total / 16384, 65536));
+  }
   if (NT > 0 && (use_reg_pass(NT, true) || use_reg_pass(NT, false))) {
     // one wave per chunk: ~4 rounds of 4 waves per CU on 256 CUs
     int64_t r = n_total / 4096;
@@ -108,7 +119,8 @@ static int64_t level_rows(const int64_t* offsets, int K, double frac, int64_t mi
 }
 
 static bool make_plan(const int64_t* offsets, int K, int p, int intercept, int rows_per_chunk,
-                      Plan& pl, double frac = 1.0, int64_t min_rows = 0) {
+                      Plan& pl, double frac = 1.0, int64_t min_rows = 0,
+                      int family = FAMILY_LOGISTIC) {
   pl.P = p + (intercept ? 1 : 0);
   pl.NT = (pl.P + 15) / 16;
   pl.T = pl.NT * (pl.NT + 1) / 2;
@@ -116,7 +128,8 @@ static bool make_plan(const int64_t* offsets, int K, int p, int intercept, int r
   // fused pass: chunk size from all rows (a warm-start level keeps the full
   // pass's chunk size: fewer, equally long chunks -- measured as fast)
   const int64_t n_total = offsets[K];
-  const int rpc = rows_per_chunk > 0 ? rows_per_chunk : auto_rows_per_chunk(n_total, pl.NT);
+  const int rpc =
+      rows_per_chunk > 0 ? rows_per_chunk : auto_rows_per_chunk(n_total, pl.NT, family);
   pl.part_chunk_begin.assign(K + 1, 0);
   pl.chunk_row0.clear();
   pl.chunk_rows.clear();
@@ -660,7 +673,7 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
                     theta, sig_inv, sig_inv_theta, loglik, iters, status, opt, stream, t_start);
 
   Plan pl;
-  make_plan(offsets, K, p, fit_intercept, opt.rows_per_chunk, pl);
+  make_plan(offsets, K, p, fit_intercept, opt.rows_per_chunk, pl, 1.0, 0, family);
   const Layout L = make_layout(pl, K);
   g_stats.n_chunks = pl.n_chunks;
 
@@ -838,7 +851,7 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
       if (n_running[ph] == 0) continue;
       const bool f64 = ph == PHASE_F64;
       pa.want_phase = ph;
-      const bool reg = use_reg_pass(q.NT, f64);
+      const bool reg = use_reg_pass(q.NT, f64, family);
       const bool ws = f64 && !reg && use_ws_pass(q.NT);
       const bool lite =
           !f64 && !reg && family == FAMILY_LOGISTIC && use_lite_pass(q.NT, p, approx_prec);
