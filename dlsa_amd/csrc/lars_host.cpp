@@ -17,6 +17,7 @@
 // computes whenever no variable has been ignored.
 #include <math.h>
 #include <string.h>
+#include <xmmintrin.h>
 
 #include <algorithm>
 #include <string>
@@ -85,6 +86,14 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
                              int32_t max_steps, double* beta_out, double* beta0_out,
                              double* aic, double* bic, int32_t* n_steps) {
   using dlsa::set_error;
+  // flush-to-zero / denormals-are-zero for the path: correlations decaying
+  // through the subnormal range made steps 10-20x slower (P = 182: 21 ms vs
+  // 3 ms at P = 150); values below 2^-1022 do not change any knot, RSS or BIC
+  struct FtzScope {
+    unsigned int saved;
+    FtzScope() : saved(_mm_getcsr()) { _mm_setcsr(saved | 0x8040); }
+    ~FtzScope() { _mm_setcsr(saved); }
+  } ftz;
   if (!Sigma0 || !b0 || P < 1 + (intercept ? 1 : 0) || !beta_out || !beta0_out || !aic || !bic ||
       !n_steps) {
     set_error("dlsa_lars_lsa: invalid arguments");
@@ -131,6 +140,8 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
 
   const size_t rows = (size_t)max_steps + 1;
   memset(beta_out, 0, sizeof(double) * rows * m);
+  std::vector<double> Csnap(rows * m);  // Cvec after each knot (knot 0: beta = 0)
+  memcpy(Csnap.data(), Cvec.data(), sizeof(double) * m);
   auto B = [&](int k, int j) -> double& { return beta_out[(size_t)k * m + j]; };
 
   std::vector<int> active, ignores;
@@ -237,6 +248,9 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
     for (int j = 0; j < m; ++j) B(k, j) = B(k - 1, j);
     for (int q = 0; q < na; ++q) B(k, active[q]) += gamhat * w[q];
     for (int j = 0; j < m; ++j) Cvec[j] -= gamhat * a[j];
+    // Cvec = Sigma (sign b - beta_k): the knot's RSS is dff . Cvec (O(m)
+    // instead of an O(m^2) quadratic form per knot at the end)
+    memcpy(&Csnap[(size_t)k * m], Cvec.data(), sizeof(double) * m);
     if (lasso && any_drop) {
       for (int q = na - 1; q >= 0; --q) {
         if (!drops[q]) continue;
@@ -290,15 +304,11 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
   const int nst = k + 1;
   *n_steps = nst;
   const double logn = log(n);
-  std::vector<double> dff(m), tmp(m);
+  std::vector<double> dff(m);
   for (int s = 0; s < nst; ++s) {
     for (int j = 0; j < m; ++j) dff[j] = sgnb[j] - B(s, j);
-    // rss = dff^T Sigma dff: e = Sigma dff as row axpys (Sigma symmetric,
-    // contiguous rows vectorise), then dff . e
-    std::fill(tmp.begin(), tmp.end(), 0.0);
-    for (int j = 0; j < m; ++j) axpy(m, dff[j], &Sig[(size_t)j * m], tmp.data());
-    double rss = 0;
-    for (int i = 0; i < m; ++i) rss += dff[i] * tmp[i];
+    // rss = dff^T Sigma dff = dff . (Sigma dff) = dff . Cvec_s (lsa.py:191-192)
+    const double rss = dot(m, dff.data(), &Csnap[(size_t)s * m]);
     int dof = 0;
     double b0s = beta0_init;
     for (int j = 0; j < m; ++j) {
