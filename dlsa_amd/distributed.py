@@ -52,16 +52,22 @@ def finish(S, v, sum_theta, K, n_global, fit_intercept=False, lars_type="lasso")
 
 
 def dlsa_fit_sharded(X, y, offsets, n_global=None, fit_intercept=False, lars_type="lasso",
-                     group=None, **fit_kw):
+                     group=None, codes=None, levels=None, **fit_kw):
     """Fit this rank's partitions on its GPU and return the global DLSA result.
 
     X, y, offsets describe the LOCAL shard (rows already on this rank's
-    device).  ``n_global`` (total rows over all ranks, for DBIC) defaults to
-    the all-reduced row count.
+    device).  With ``codes``/``levels`` X holds the numeric columns of the
+    categorical-code layout (``logistic_model_batched_categorical``).
+    ``n_global`` (total rows over all ranks, for DBIC) defaults to the
+    all-reduced row count.
     """
-    from .models import logistic_model_batched
+    from .models import logistic_model_batched, logistic_model_batched_categorical
 
-    fit = logistic_model_batched(X, y, offsets, fit_intercept=fit_intercept, **fit_kw)
+    if codes is not None:
+        fit = logistic_model_batched_categorical(X, codes, y, offsets, levels,
+                                                 fit_intercept=fit_intercept, **fit_kw)
+    else:
+        fit = logistic_model_batched(X, y, offsets, fit_intercept=fit_intercept, **fit_kw)
     buf = reduce_partitions_device(fit)
     combine(buf, group)
     S, v, st, K = split_reduced(buf.cpu().numpy(), fit.P)

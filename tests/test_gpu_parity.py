@@ -545,3 +545,24 @@ def test_categorical_invalid_code_fails_loudly(torch_cuda, M):
     codes[17, 1] = 4  # levels[1] = 4 -> valid codes 0..3
     with pytest.raises(DlsaHipError, match="level codes"):
         M.logistic_model_batched_categorical(Xn, codes, y, off, [3, 4], fit_intercept=True)
+
+
+def test_dlsa_fit_sharded_dense_and_categorical(torch_cuda, M):
+    """The one-rank path of dlsa_fit_sharded (fit -> HBM pre-reduction -> WLSE
+    -> LARS/DBIC) for both layouts: WLSE and the DBIC support match the oracle
+    on the dense expansion."""
+    from dlsa_amd.distributed import dlsa_fit_sharded
+
+    Xn, codes, y, off = _cat_case(4, [5, 7], 4, seed=21)
+    levels = [5, 7]
+    X = O.expand_codes(Xn, codes, levels)
+    th, S, St, ll, it = O.logistic_fit_partitions(X, y, off, fit_intercept=True)
+    wlse, oneshot, Ssum = O.dlsa_mapred(th, S, St)
+    for kw in (dict(X=X), dict(X=Xn, codes=codes, levels=levels)):
+        Xa = kw.pop("X")
+        res = dlsa_fit_sharded(Xa, y, off, fit_intercept=True, **kw)
+        assert _rel(res["wlse"], wlse) < REL
+        assert _rel(res["oneshot"], oneshot) < REL
+        _, b_bic = O.dlsa(Ssum, wlse, int(off[-1]), fit_intercept=True)
+        sup_ref = np.nonzero(np.asarray(b_bic)[1:])[0] + 1
+        assert res["dbic_support"].tolist() == sup_ref.tolist()
