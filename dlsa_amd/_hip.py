@@ -14,7 +14,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdlsa_hip.so")
+# DLSA_LIB: profiling variants (tools/build_variants.sh); default the in-tree build
+LIB_PATH = os.environ.get("DLSA_LIB") or os.path.join(_HERE, "libdlsa_hip.so")
 
 DLSA_OK = 0
 STATUS_NAMES = {0: "ok", 1: "maxiter", 2: "singular", 3: "empty", 4: "nonfinite", 5: "missing_level"}

@@ -1042,7 +1042,13 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
     const int64_t per = std::max<int64_t>(1, 512 / std::max(K, 1));
     return (int)std::max<int64_t>(1024, std::min<int64_t>((nmax + per - 1) / per, 1 << 24));
   };
+  // no warm-start levels: every categorical pass is exact and cheap, so the
+  // prefix levels' extra launches and host round trips cost more than the
+  // full-row passes they save (config 3: 11.2 ms per fit without levels,
+  // 14.9 ms with); DLSA_WARM_START=1 restores them (profiling knob)
   std::vector<Plan> plans;
+  opt.warm_start = 0;
+  if (const char* e = getenv("DLSA_WARM_START")) opt.warm_start = atoi(e);
   if (opt.warm_start) {
     const int64_t min_rows = std::max<int64_t>(2048, 64LL * P);
     for (double frac : {1.0 / 16.0, 1.0 / 4.0}) {

@@ -34,6 +34,13 @@
 
 #include "dlsa_internal.hpp"
 
+// Profiling-only ablation bits (tools/build_variants.sh cat*; product build 0):
+// 1 no numeric x dummy histogram adds, 2 no pair adds, 4 no gradient adds,
+// 8 no numeric register block, 16 no slab-epilogue lookups.
+#ifndef DLSA_CAT_ABLATE
+#define DLSA_CAT_ABLATE 0
+#endif
+
 namespace dlsa {
 
 __device__ __forceinline__ void lds_add(double* p, double v) {
@@ -145,7 +152,7 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
     llacc += yv * e - (fmax(e, 0.0) + log1p(ea));
 
 #pragma unroll
-    for (int i = 0; i < QN; ++i) {
+    for (int i = 0; i < QN && !(DLSA_CAT_ABLATE & 8); ++i) {
       gacc[i] = fma(res, xv[i], gacc[i]);
       const double wxi = w * xv[i];
 #pragma unroll
@@ -158,18 +165,20 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
       if (f < F && cv[f] > 0) {
         const int slot = (lane & t_ndrep[f]) * t_nlev[f] + cv[f] - 1;
         double* h = hist + t_ndoff[f] + slot * Qw;
-        lds_add(h, w);
+        if constexpr (!(DLSA_CAT_ABLATE & 1)) {
+          lds_add(h, w);
 #pragma unroll
-        for (int i = 0; i < QN; ++i)  // numeric columns (register index compile-time)
-          if (i >= ic && i < Qn) lds_add(h + 1 + (i - ic), w * xv[i]);
-        lds_add(hist + t_goff[f] + slot, res);
+          for (int i = 0; i < QN; ++i)  // numeric columns (register index compile-time)
+            if (i >= ic && i < Qn) lds_add(h + 1 + (i - ic), w * xv[i]);
+        }
+        if constexpr (!(DLSA_CAT_ABLATE & 4)) lds_add(hist + t_goff[f] + slot, res);
       }
     }
 #pragma unroll
     for (int f = 0; f < FM; ++f)
 #pragma unroll
       for (int g = f + 1; g < FM; ++g) {
-        if (g < F && cv[f] > 0 && cv[g] > 0) {
+        if (!(DLSA_CAT_ABLATE & 2) && g < F && cv[f] > 0 && cv[g] > 0) {
           const int pi = cat_pair(f, g, F);
           const int rep = lane & t_prrep[pi];
           lds_add(hist + t_proff[pi] + (rep * t_nlev[f] + cv[f] - 1) * t_nlev[g] + cv[g] - 1, w);
@@ -234,7 +243,7 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
     const int J = t - I * (I + 1) / 2;
     const int gi = 16 * I + (pos >> 4), gj = 16 * J + (pos & 15);
     double v = 0.0;
-    if (gi < P && gj <= gi) {
+    if (!(DLSA_CAT_ABLATE & 16) && gi < P && gj <= gi) {
       if (gi < Qn) {
         v = fin[gi * (gi + 1) / 2 + gj];
       } else {

@@ -349,8 +349,7 @@ def logistic_model_batched(X, y, offsets, fit_intercept=False, center=None, scal
 
 def logistic_model_batched_categorical(Xn, codes, y, offsets, levels, fit_intercept=False,
                                        center=None, scale=None, max_iter=100, tol=1e-10,
-                                       record_timing=False, rows_per_chunk=0, warm_start=True,
-                                       device=None):
+                                       record_timing=False, rows_per_chunk=0, device=None):
     """Batched local logistic fit on the categorical-code layout (the dummy
     branch of dlsa/models.py:56-91, BASELINE config 3) without materialising
     the dummy matrix: the one-hot blocks of X^T W X are LDS histograms in the
@@ -399,7 +398,6 @@ def logistic_model_batched_categorical(Xn, codes, y, offsets, levels, fit_interc
     opt = _hip.default_options()
     opt.record_timing = 1 if record_timing else 0
     opt.rows_per_chunk = int(rows_per_chunk)
-    opt.warm_start = 1 if warm_start else 0
     rc = lib.dlsa_logistic_fit_categorical(
         _ptr(Xd), _ptr(cd8), _ptr(yd), offs.ctypes.data_as(ctypes.c_void_p), K, q, F,
         lv.ctypes.data_as(ctypes.c_void_p), int(bool(fit_intercept)), _ptr(cen), _ptr(sca),

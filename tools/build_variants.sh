@@ -10,6 +10,13 @@ for v in "$@"; do
     ablate2) D=DLSA_ABLATE=2 ;;
     ablate3) D=DLSA_ABLATE=3 ;;
     ablate4) D=DLSA_ABLATE=4 ;;
+    cat1) D=DLSA_CAT_ABLATE=1 ;;
+    cat2) D=DLSA_CAT_ABLATE=2 ;;
+    cat4) D=DLSA_CAT_ABLATE=4 ;;
+    cat7) D=DLSA_CAT_ABLATE=7 ;;
+    cat15) D=DLSA_CAT_ABLATE=15 ;;
+    cat16) D=DLSA_CAT_ABLATE=16 ;;
+    cat31) D=DLSA_CAT_ABLATE=31 ;;
     *) echo "unknown variant $v"; exit 1 ;;
   esac
   python -c "from dlsa_amd.build import build; print(build(force=True, out='tools/_variants/libdlsa_hip_$v.so', defines=['$D']))"
