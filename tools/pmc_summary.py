@@ -7,14 +7,19 @@ roofline.traffic.  HBM bytes = 2 x FETCH_SIZE (gfx950 reports half the bytes
 of a 16 B/lane streaming read, MI355X_MICROARCH.md "HBM / rocprofv3") +
 WRITE_SIZE, both in KB (x1024).
 
-Usage: python tools/pmc_summary.py <tag> <out-prefix> <config> <n> <p> <kernel-label>
+Usage: python tools/pmc_summary.py <tag> <out-prefix> <config> <n> <p> <kernel-label> [regex]
+
+<regex> selects the dispatches of the roofline kernel (default: the config-2
+bf16 cooperative pass, irls_coop_kernel<.., 0, false, ..>).
 """
 import csv
 import json
 import os
+import re
 import sys
 
 tag, prefix, config, n, p, label = sys.argv[1:7]
+pattern = re.compile(sys.argv[7] if len(sys.argv) > 7 else r"irls_coop_kernel<.*, 0, false")
 root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 base = os.path.join(root, "gpurun_out", tag)
 rows = []
@@ -23,8 +28,8 @@ for i in range(1, 5):
     if not os.path.exists(f):
         continue
     for r in csv.DictReader(open(f)):
-        if "irls_" in r["Kernel_Name"] or "wide_" in r["Kernel_Name"]:
-            rows.append({"pass": i, "dispatch": r["Dispatch_Id"], "kernel": r["Kernel_Name"][:80],
+        if any(t in r["Kernel_Name"] for t in ("irls_", "wide_", "cat_", "part_")):
+            rows.append({"pass": i, "dispatch": r["Dispatch_Id"], "kernel": r["Kernel_Name"][:120],
                          "grid": r["Grid_Size"], "counter": r["Counter_Name"],
                          "value": r["Counter_Value"],
                          "ms": (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6})
@@ -37,7 +42,7 @@ with open(out_csv, "w", newline="") as fh:
 # bf16 (approximate) pass dispatches: the kernel template with HMODE 0
 def pick(counter):
     return [float(r["value"]) for r in rows
-            if r["counter"] == counter and "irls_coop_kernel" in r["kernel"] and ", 0, false" in r["kernel"]]
+            if r["counter"] == counter and pattern.search(r["kernel"])]
 fetch, write = pick("FETCH_SIZE"), pick("WRITE_SIZE")
 assert fetch and len(fetch) == len(write), (len(fetch), len(write))
 per_launch = (2 * sum(fetch) + sum(write)) * 1024 / len(fetch)
