@@ -56,6 +56,8 @@ def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()
         def compile_one(src):
             obj = os.path.join(tmp, os.path.splitext(src)[0] + ".o")
             cmd = common + ["-c", os.path.join(CSRC, src), "-o", obj]
+            if src.endswith(".cpp"):  # host-only code (LARS): AVX2/FMA vector loops (x86-64-v3)
+                cmd += ["-march=x86-64-v3"]
             if verbose:
                 print(" ".join(cmd), flush=True)
             return obj, subprocess.run(cmd, capture_output=True, text=True)
