@@ -566,3 +566,17 @@ def test_dlsa_fit_sharded_dense_and_categorical(torch_cuda, M):
         _, b_bic = O.dlsa(Ssum, wlse, int(off[-1]), fit_intercept=True)
         sup_ref = np.nonzero(np.asarray(b_bic)[1:])[0] + 1
         assert res["dbic_support"].tolist() == sup_ref.tolist()
+
+
+@pytest.mark.parametrize("q,levels,fi", [(0, [6, 4], True), (5, [], True), (3, [1, 5], False)])
+def test_categorical_edge_layouts(torch_cuda, M, q, levels, fi):
+    """Factors only (q = 0), no factors (F = 0: the numeric block alone), and a
+    one-level factor (no dummy columns): same estimates as the oracle on the
+    dense expansion."""
+    Xn, codes, y, off = _cat_case(q, levels, 2, seed=5 + q)
+    fit = M.logistic_model_batched_categorical(Xn, codes, y, off, levels, fit_intercept=fi)
+    X = O.expand_codes(Xn, codes, levels)
+    th, S, St, ll, it = O.logistic_fit_partitions(X, y, off, fit_intercept=fi)
+    assert (fit.status.cpu().numpy() == 0).all(), fit.status
+    assert _rel(fit.theta.cpu(), th) < REL
+    assert _rel(fit.sig_inv.cpu(), S) < REL
