@@ -16,6 +16,18 @@
 
 #include "dlsa_internal.hpp"
 
+// Profiling-only phase timestamps of partition 0 (tools/build_variants.sh
+// solveprof; product build 0): printf of shader-clock deltas per phase.
+#ifndef DLSA_SOLVE_PROFILE
+#define DLSA_SOLVE_PROFILE 0
+#endif
+#if DLSA_SOLVE_PROFILE
+#define SOLVE_MARK(i) \
+  if (k == 0 && tid == 0) tmark[i] = clock64();
+#else
+#define SOLVE_MARK(i)
+#endif
+
 namespace dlsa {
 
 __device__ __forceinline__ double block_max(double v, double* red) {
@@ -68,6 +80,10 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
   // partials_sum_kernel (fixed chunk order)
   const int cb = a.part_chunk_begin[k], ce = min(a.part_chunk_begin[k + 1], cb + 1);
   const int phase = a.phase[k];
+#if DLSA_SOLVE_PROFILE
+  long long tmark[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+  SOLVE_MARK(0)
 
   // 1. assemble: thread tid owns element (tile t, position tid) of every
   //    tile.  Only the
@@ -144,6 +160,7 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
     return;
   }
 
+  SOLVE_MARK(1)
   // 3. publish the information matrix at the evaluation point --------------
   if (!a.subsample) {
     double* S = a.sig_inv + (int64_t)k * P * P;
@@ -165,6 +182,7 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
   //        A_IJ -= L_Ib L_Jb^T (16x16 tiles, 4 k-steps of 4 columns).
   //    Three barriers per 16 columns (was one per column with a serial
   //    per-thread row update).
+  SOLVE_MARK(2)
   if (tid == 0) red[5] = 0.0;
   __syncthreads();
   bool ok = true;
@@ -271,41 +289,74 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
     return;
   }
 
+  SOLVE_MARK(3)
   // 5. triangular solves L z = g, L^T d = z by wave 0 (no barriers: lane l
-  //    holds z[l + 64 r]; the pivot is broadcast by shuffle)
+  //    holds z[l + 64 r]).  The pivot's owner lane scales it by 1 / L_jj and
+  //    v_readlane broadcasts it (no LDS round trip on the recurrence); the
+  //    L entries of 4 steps are read ahead, off the dependency chain
+  //    (P = 182: 239k -> see DESIGN.md cycles per solve pair).  Same
+  //    arithmetic, in the same order, as a per-step shuffle.
   if (wid == 0) {
-    double zr[R];
+    constexpr int U = 4;
+    double zr[R], ir[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) zr[r] = lane + 64 * r < P ? g[lane + 64 * r] : 0.0;
-    for (int j = 0; j < P; ++j) {
-      double piv = 0.0;
+    for (int r = 0; r < R; ++r) {
+      const int i = lane + 64 * r;
+      zr[r] = i < P ? g[i] : 0.0;
+      ir[r] = i < P ? invd[i] : 0.0;
+    }
+    for (int j0 = 0; j0 < P; j0 += U) {
+      double hv[U][R];
 #pragma unroll
-      for (int r = 0; r < R; ++r)
-        if ((j >> 6) == r) piv = zr[r];
-      const double zj = __shfl(piv, j & 63) * invd[j];
+      for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int i = lane + 64 * r;
-        if (i == j)
-          zr[r] = zj;
-        else if (i > j && i < P)
-          zr[r] -= H[tri(i, j)] * zj;
+        for (int r = 0; r < R; ++r) {
+          const int i = lane + 64 * r, j = j0 + u;
+          hv[u][r] = (j < P && i > j && i < P) ? H[tri(i, j)] : 0.0;
+        }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int j = j0 + u;
+        if (j < P) {  // wave-uniform
+          double zs = 0.0;
+#pragma unroll
+          for (int r = 0; r < R; ++r)
+            if ((j >> 6) == r) zs = zr[r] * ir[r];
+          const double zj = readlane_f64(zs, j & 63);
+#pragma unroll
+          for (int r = 0; r < R; ++r) {  // branch-free: hv = 0 off the active rows
+            const int i = lane + 64 * r;
+            const double upd = fma(-hv[u][r], zj, zr[r]);
+            zr[r] = i == j ? zj : upd;
+          }
+        }
       }
     }
-    for (int j = P - 1; j >= 0; --j) {
-      double piv = 0.0;
+    for (int j0 = P - 1; j0 >= 0; j0 -= U) {
+      double hv[U][R];
 #pragma unroll
-      for (int r = 0; r < R; ++r)
-        if ((j >> 6) == r) piv = zr[r];
-      const double zj = __shfl(piv, j & 63) * invd[j];
-      const double* lj = H + tri(j, 0);
+      for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int i = lane + 64 * r;
-        if (i == j)
-          zr[r] = zj;
-        else if (i < j)
-          zr[r] -= lj[i] * zj;
+        for (int r = 0; r < R; ++r) {
+          const int i = lane + 64 * r, j = j0 - u;
+          hv[u][r] = (j >= 0 && i < j) ? H[tri(j, 0) + i] : 0.0;
+        }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int j = j0 - u;
+        if (j >= 0) {  // wave-uniform
+          double zs = 0.0;
+#pragma unroll
+          for (int r = 0; r < R; ++r)
+            if ((j >> 6) == r) zs = zr[r] * ir[r];
+          const double zj = readlane_f64(zs, j & 63);
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const int i = lane + 64 * r;
+            const double upd = fma(-hv[u][r], zj, zr[r]);
+            zr[r] = i == j ? zj : upd;
+          }
+        }
       }
     }
 #pragma unroll
@@ -314,6 +365,12 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
   }
   __syncthreads();
 
+  SOLVE_MARK(4)
+#if DLSA_SOLVE_PROFILE
+  if (k == 0 && tid == 0)
+    printf("[solve-profile] P=%d assemble %lld publish %lld cholesky %lld trisolve %lld\n", P,
+           tmark[1] - tmark[0], tmark[2] - tmark[1], tmark[3] - tmark[2], tmark[4] - tmark[3]);
+#endif
   // 6. update + convergence ------------------------------------------------
   double dm = 0.0, tm = 0.0, tg = 0.0;
   double* tp = a.theta_prev + (int64_t)k * P;

@@ -16,6 +16,7 @@ for v in "$@"; do
     cat7) D=DLSA_CAT_ABLATE=7 ;;
     cat15) D=DLSA_CAT_ABLATE=15 ;;
     cat16) D=DLSA_CAT_ABLATE=16 ;;
+    solveprof) D=DLSA_SOLVE_PROFILE=1 ;;
     cat31) D=DLSA_CAT_ABLATE=31 ;;
     *) echo "unknown variant $v"; exit 1 ;;
   esac
