@@ -30,6 +30,16 @@
 
 namespace dlsa {
 
+// Broadcast lane `l` (wave-uniform, here a compile-time column index) of a
+// double with two v_readlane: no LDS round trip (ds_bpermute) on the
+// dependency chains of the small factorizations and solves below.
+__device__ __forceinline__ double bcast_f64(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
+
+
 typedef double d4w __attribute__((ext_vector_type(4)));
 
 namespace {
@@ -754,14 +764,14 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
       bool ok = true;
 #pragma unroll
       for (int j = 0; j < CB; ++j) {
-        const double d = __shfl(row[j], j);
+        const double d = bcast_f64(row[j], j);
         ok = ok && d > 0.0 && isfinite(d);
         const double ljj = sqrt(d);
         if (i == j) row[j] = ljj;
         if (i > j) row[j] = row[j] / ljj;
 #pragma unroll
         for (int c = j + 1; c < CB; ++c) {
-          const double lcj = __shfl(row[j], c);  // L[c][j]
+          const double lcj = bcast_f64(row[j], c);  // L[c][j]
           if (i >= c) row[c] -= row[j] * lcj;
         }
       }
@@ -854,7 +864,7 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
 #pragma unroll
       for (int c = 0; c < CB; ++c) {
         if (i == c) zi = zi / lrow[c];
-        const double zc = __shfl(zi, c);
+        const double zc = bcast_f64(zi, c);
         if (i > c) zi -= lrow[c] * zc;
       }
       if (lane < 32) z[jb + i] = zi;
@@ -892,7 +902,7 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
 #pragma unroll
       for (int r = CB - 1; r >= 0; --r) {
         if (c == r) v = v / lcol[r];
-        const double dr = __shfl(v, r);
+        const double dr = bcast_f64(v, r);
         if (c < r) v -= lcol[r] * dr;
       }
       if (lane < 32) z[jb + c] = v;
