@@ -210,7 +210,9 @@ def encode_categorical(sample_df, Y_name, dummy_info, dummy_factors_baseline=())
         import pandas as pd
 
         inv, uniq = pd.factorize(df[f], sort=False)  # one name per distinct value
-        mapped = np.array([lut.get(f"{f}_{u}", -1) for u in uniq], dtype=np.int64)
+        # a missing value (factorize code -1) has no dummy column in
+        # pd.get_dummies (dummy_na=False): all-zero block = code 0
+        mapped = np.array([lut.get(f"{f}_{u}", -1) for u in uniq] + [0], dtype=np.int64)
         c = mapped[inv] if n else np.zeros(0, dtype=np.int64)
         if (c < 0).any():
             unknown = True

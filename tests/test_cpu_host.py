@@ -304,3 +304,21 @@ def test_ingest_fails_loudly_without_gpu():
 
     with pytest.raises(DlsaHipError):
         repartition(torch.zeros(4, dtype=torch.int32), 2, torch.zeros((4, 2)))
+
+
+def test_encode_categorical_missing_value_is_all_zero_block():
+    """pd.get_dummies (dummy_na=False) gives a missing factor value no column:
+    the encoder maps it to code 0 (the all-zero dummy block)."""
+    import pandas as pd
+
+    from dlsa_amd.models import encode_categorical
+
+    df = pd.DataFrame({"partition_id": [0.0] * 6, "y": [0, 1, 0, 1, 1, 0.0],
+                       "F": ["a", "b", None, "c", "a", "b"], "x": [1, 2, 3, 4, 5, 6.0]})
+    di = {"factor_selected": {"F": ["a", "b", "c"]}, "factor_dropped": {"F": []},
+          "factor_selected_names": {"F": ["F_a", "F_b", "F_c"]}}
+    e = encode_categorical(df, "y", di, ["F_a"])
+    ref = pd.get_dummies(df, columns=["F"]).drop(columns=["F_a", "partition_id", "y"])
+    assert e["cols"] == list(ref.columns)
+    assert np.array_equal(O.expand_codes(e["Xn"], e["codes"], e["levels"]),
+                          ref.to_numpy(dtype=np.float64))
