@@ -112,6 +112,37 @@ static int64_t rows_used(int64_t nk, double frac, int64_t min_rows) {
   if (frac >= 1.0) return nk;
   return std::min(nk, std::max(min_rows, (int64_t)std::ceil(frac * (double)nk)));
 }
+// warm-start row-prefix fractions (ascending, each < 1); DLSA_LEVELS="a,b,..."
+// overrides (schedule sweeps, tools/level_sweep.sh), DLSA_LEVELS="" disables.
+// A level using more than half of all rows is skipped, so "x,0.5" runs as
+// "x" alone at config 2 (odd n_k round up).  Fused pass (config 2,
+// profiles/r01m_level_sweep.jsonl, 6-step means): one 1/16 level at a
+// 0.2-relative step 101 ms per fit vs 110 ms for 1/16, 1/4 at 0.1 (6 bf16 +
+// 1 fp64 launches instead of 9 + 1: the 1/4 level's passes cost more than
+// the one full pass they save).  Wide path (config 5): 1/16, 1/4 at 0.1
+// kept -- the alternatives were within noise or triggered a second fp64
+// Gram pass (36 ms).
+static std::vector<double> warm_level_fracs(bool fused) {
+  std::vector<double> f = fused ? std::vector<double>{1.0 / 16.0}
+                                : std::vector<double>{1.0 / 16.0, 1.0 / 4.0};
+  if (const char* e = getenv("DLSA_LEVELS")) {
+    f.clear();
+    for (const char* s = e; *s;) {
+      char* end = nullptr;
+      const double v = strtod(s, &end);
+      if (end == s) break;
+      if (v > 0.0 && v < 1.0) f.push_back(v);
+      s = (*end == ',') ? end + 1 : end;
+    }
+  }
+  return f;
+}
+// a level stops once its max relative step is below this; DLSA_LEVEL_TOL overrides
+static double warm_level_tol(bool fused) {
+  if (const char* e = getenv("DLSA_LEVEL_TOL")) return atof(e);
+  return fused ? 0.2 : 0.1;
+}
+
 static int64_t level_rows(const int64_t* offsets, int K, double frac, int64_t min_rows) {
   int64_t n = 0;
   for (int k = 0; k < K; ++k) n += std::max<int64_t>(0, rows_used(offsets[k + 1] - offsets[k], frac, min_rows));
@@ -507,7 +538,7 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
   std::vector<WidePlans> plans;
   if (family == FAMILY_LOGISTIC && opt.warm_start) {
     const int64_t min_rows = std::max<int64_t>(2048, 64LL * P);
-    for (double frac : {1.0 / 16.0, 1.0 / 4.0}) {
+    for (double frac : warm_level_fracs(false)) {
       WidePlans q;
       make_wide_plans(offsets, K, p, fit_intercept, opt.rows_per_chunk, q, frac, min_rows);
       int64_t rows = 0;
@@ -579,7 +610,7 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
       n_running[1] = h_cnt[1];
     }
     sa.subsample = final_level ? 0 : 1;
-    sa.level_tol = 0.1;
+    sa.level_tol = warm_level_tol(false);
     sa.switch_tol = final_level ? opt.switch_tol : 0.0;
     const int it_end = final_level ? max_iter : std::min(max_iter, it + 10);
     for (; it < it_end && (n_running[0] + n_running[1]) > 0 && q.rows.n_chunks > 0; ++it) {
@@ -734,7 +765,7 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
   std::vector<Plan> plans;
   if (family == FAMILY_LOGISTIC && opt.warm_start) {
     const int64_t min_rows = std::max<int64_t>(2048, 64LL * pl.P);
-    for (double frac : {1.0 / 16.0, 1.0 / 4.0}) {
+    for (double frac : warm_level_fracs(true)) {
       Plan q;
       make_plan(offsets, K, p, fit_intercept, opt.rows_per_chunk, q, frac, min_rows);
       int64_t rows = 0;
@@ -843,7 +874,7 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
     // the prefix MLE is ~sqrt(P/n) from the full one (max step ~0.2 entering
     // the full level at config 2), so a level stops at a 0.1-relative step
     // (measured max steps: 0.93, 0.42, 0.15 | 0.49, 0.04 | then full rows)
-    sa.level_tol = 0.1;
+    sa.level_tol = warm_level_tol(true);
     sa.switch_tol = final_level ? opt.switch_tol : 0.0;
     const int it_end = final_level ? max_iter : std::min(max_iter, it + 10);
   for (; it < it_end && (n_running[0] + n_running[1]) > 0 && q.n_chunks > 0; ++it) {
@@ -1051,7 +1082,7 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
   if (const char* e = getenv("DLSA_WARM_START")) opt.warm_start = atoi(e);
   if (opt.warm_start) {
     const int64_t min_rows = std::max<int64_t>(2048, 64LL * P);
-    for (double frac : {1.0 / 16.0, 1.0 / 4.0}) {
+    for (double frac : warm_level_fracs(true)) {
       Plan qn;
       const int64_t lr = level_rows(offsets, K, frac, min_rows);
       make_plan(offsets, K, P - ic, ic, cat_rpc(frac, min_rows), qn, frac, min_rows);
@@ -1211,7 +1242,7 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
       n_running = h_cnt[0] + h_cnt[1];
     }
     sa.subsample = final_level ? 0 : 1;
-    sa.level_tol = 0.1;
+    sa.level_tol = warm_level_tol(true);
     sa.switch_tol = 0.0;
     const int it_end = final_level ? max_iter : std::min(max_iter, it + 10);
     for (; it < it_end && n_running > 0 && qn.n_chunks > 0; ++it) {
