@@ -871,9 +871,9 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
       n_running[1] = h_cnt[1];
     }
     sa.subsample = final_level ? 0 : 1;
-    // the prefix MLE is ~sqrt(P/n) from the full one (max step ~0.2 entering
-    // the full level at config 2), so a level stops at a 0.1-relative step
-    // (measured max steps: 0.93, 0.42, 0.15 | 0.49, 0.04 | then full rows)
+    // the prefix MLE is ~sqrt(P/n) from the full one (max step ~0.35 entering
+    // the full level at config 2), so a level need not converge: it stops at
+    // a 0.2-relative step (warm_level_tol)
     sa.level_tol = warm_level_tol(true);
     sa.switch_tol = final_level ? opt.switch_tol : 0.0;
     const int it_end = final_level ? max_iter : std::min(max_iter, it + 10);
