@@ -298,8 +298,8 @@ def main():
                     "avg_launch_ms": ms32 / n32}
         else:
             achieved = rows64 * mfma_flops_per_row / (ms64 * 1e-3) / 1e12
-            kname = (f"irls_reg_kernel<NT={NT},fp64> (OLS register pass)"
-                     if family == "ols" and NT <= 7 else f"irls_coop_kernel<NT={NT},fp64 Hessian>")
+            kname = (f"irls_wave_kernel<NT={NT},fp64> (per-wave exact pass)" if NT <= 8
+                     else f"irls_coop_kernel<NT={NT},fp64 Hessian>")
             roof = {"kernel": kname, "bound": "mfma",
                     "achieved": achieved, "peak": FP64_MFMA_PEAK_TF, "unit": "TFLOP/s",
                     "frac": achieved / FP64_MFMA_PEAK_TF, "traffic": None,

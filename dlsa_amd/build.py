@@ -18,11 +18,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libdlsa_hip.so")
-SOURCES = (["irls_pass.hip", "irls_coop.hip"] + [f"irls_coop_g{i}.hip" for i in range(1, 7)] +
-           ["irls_reg.hip"] + [f"irls_reg_g{i}.hip" for i in range(1, 4)] +
-           ["irls_ws.hip"] + [f"irls_ws_g{i}.hip" for i in range(1, 3)] + ["irls_lite.hip"] +
+SOURCES = (["irls_coop.hip"] + [f"irls_coop_g{i}.hip" for i in range(1, 7)] +
+           ["irls_wave.hip", "irls_wave_g2.hip"] +
            ["wide_pass.hip", "cat_pass.hip", "partition_rows.hip", "eval_pass.hip", "newton_solve.hip", "aux_kernels.hip", "capi.hip", "lars_host.cpp"])
-HEADERS = ["dlsa_internal.hpp", "irls_coop_impl.hpp", "irls_reg_impl.hpp", "irls_ws_impl.hpp", "irls_lite_impl.hpp", os.path.join("..", "..", "include", "dlsa_hip.h")]
+HEADERS = ["dlsa_internal.hpp", "irls_coop_impl.hpp", "irls_wave_impl.hpp", os.path.join("..", "..", "include", "dlsa_hip.h")]
 ARCH = os.environ.get("DLSA_OFFLOAD_ARCH", "gfx950")
 
 

@@ -7,7 +7,10 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <map>
+#include <mutex>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "dlsa_internal.hpp"
@@ -18,6 +21,20 @@ static thread_local std::string g_last_error;
 static thread_local dlsa_fit_stats g_stats;
 
 void set_error(const std::string& msg) { g_last_error = msg; }
+
+hipError_t ensure_max_lds(const void* kernel, int bytes) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  static std::mutex mu;
+  static std::map<std::pair<const void*, int>, int> done;  // (kernel, device) -> bytes set
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = done.find({kernel, dev});
+  if (it != done.end() && it->second >= bytes) return hipSuccess;
+  e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e == hipSuccess) done[{kernel, dev}] = bytes;
+  return e;
+}
 
 #define DLSA_HIP_TRY(expr)                                                            \
   do {                                                                                \
@@ -40,67 +57,16 @@ struct Plan {
   std::vector<int32_t> chunk_rows, chunk_part, part_chunk_begin;
 };
 
-static bool use_perwave_pass() {
-  const char* e = getenv("DLSA_PASS");
-  return e && strcmp(e, "perwave") == 0;
-}
-
-// Pass kernel of a precision phase: the register-streaming pass (one wave
-// per chunk, all tiles in registers; P <= 112) or the cooperative LDS pass.
-// DLSA_PASS_F64 / DLSA_PASS_LOWP = reg | coop override the default.
-// Default: the register pass for the OLS (gaussian) fp64 pass -- measured at
-// config 4 (p = 64, NT = 4): 16.8 ms vs 22.4 ms cooperative, as every tile of
-// X^T X fits one wave's registers and there is no row-phase transcendental
-// work to overlap; the cooperative pass elsewhere (config 2 fp64: 33.1 vs
-// 38.9 ms reg).
-static bool use_reg_pass(int NT, bool f64, int family = FAMILY_LOGISTIC) {
-  if (NT > kRegMaxNT || use_perwave_pass()) return false;
-  const char* e = getenv(f64 ? "DLSA_PASS_F64" : "DLSA_PASS_LOWP");
-  if (e) return strcmp(e, "reg") == 0;
-  return f64 && family == FAMILY_GAUSSIAN;
-}
-
-// fp64 passes: the wave-specialised kernel (P <= 128) unless
-// DLSA_PASS_F64 = coop | reg
-static bool use_ws_pass(int NT) {
-  if (NT > kWsMaxNT || use_perwave_pass()) return false;
-  const char* e = getenv("DLSA_PASS_F64");
-  if (e) return strcmp(e, "ws") == 0;
-  return false;
-}
-
-// bf16 approximate passes: the light-weight kernel when its in-place operand
-// images fit (P <= 128, P <~ 2p), unless DLSA_PASS_LOWP = coop | reg
-static bool use_lite_pass(int NT, int p, int prec) {
-  if (prec != PREC_BF16 || !lite_fits(NT, p) || use_perwave_pass()) return false;
-  const char* e = getenv("DLSA_PASS_LOWP");
-  if (e) return strcmp(e, "lite") == 0;
-  return false;
-}
-
-static int auto_rows_per_chunk(int64_t n_total, int NT = 0, int family = FAMILY_LOGISTIC) {
+// Chunking: ~8192 chunks of consecutive rows of one partition.  The
+// cooperative pass runs one 4-wave workgroup per chunk (2 per CU: 512 in
+// flight), the per-wave fp64 pass one wave per chunk (4 per CU: 1024 in
+// flight), so a launch is whole rounds of either; the partial tiles
+// (T * 2 KiB per chunk) stay ~1 % of the X traffic.  Measured at config 2
+// (cooperative bf16 / fp64 pass ms): 1024 chunks 22.0 / 42.5, 2048 19.4 /
+// 36.6, 4096 18.2 / 34.7, 8192 17.4 / 33.2, 16384 17.0 / 32.8 (but the Newton
+// solve reads every chunk's partial tiles: 0.65 -> 0.74 ms per iteration).
+static int auto_rows_per_chunk(int64_t n_total) {
   if (const char* e = getenv("DLSA_ROWS_PER_CHUNK")) return std::max(64, atoi(e));
-  if (NT > 0 && family == FAMILY_GAUSSIAN && use_reg_pass(NT, true, family)) {
-    // OLS register pass: ~16k one-wave chunks (config 4 sweep, ms per pass /
-    // per fit: 2080 chunks 21.6, 4224 18.5, 8320 16.7 / 17.8, 12.5k 16.1 / 17.4,
-    // 16.7k 15.7 / 16.9 -- the solve sums more chunk partials)
-    return (int)std::max<int64_t>(1024, std::min<int64_t>(n_total / 16384, 65536));
-  }
-  if (NT > 0 && (use_reg_pass(NT, true) || use_reg_pass(NT, false))) {
-    // one wave per chunk: ~4 rounds of 4 waves per CU on 256 CUs
-    int64_t r = n_total / 4096;
-    return (int)std::max<int64_t>(1024, std::min<int64_t>(r, 65536));
-  }
-  if (use_perwave_pass()) {
-    // one wave per chunk: ~8 waves per CU-slot round on 256 CUs
-    int64_t r = n_total / 4096;
-    r = std::max<int64_t>(256, std::min<int64_t>(r, 8192));
-    return (int)r;
-  }
-  // one 4-wave workgroup per chunk, ~8192 chunks: measured at config 2
-  // (bf16 / fp64 pass ms) 1024 chunks 22.0 / 42.5, 2048 19.4 / 36.6,
-  // 4096 18.2 / 34.7, 8192 17.4 / 33.2, 16384 17.0 / 32.8 (but the Newton
-  // solve reads every chunk's partial tiles: 0.65 -> 0.74 ms per iteration)
   int64_t r = n_total / 8192;
   r = std::max<int64_t>(1024, std::min<int64_t>(r, 131072));
   return (int)r;
@@ -137,6 +103,8 @@ static std::vector<double> warm_level_fracs(bool fused) {
   }
   return f;
 }
+// iteration budget of one warm-start level (its own, not part of max_iter)
+constexpr int kLevelIters = 10;
 // a level stops once its max relative step is below this; DLSA_LEVEL_TOL overrides
 static double warm_level_tol(bool fused) {
   if (const char* e = getenv("DLSA_LEVEL_TOL")) return atof(e);
@@ -150,8 +118,7 @@ static int64_t level_rows(const int64_t* offsets, int K, double frac, int64_t mi
 }
 
 static bool make_plan(const int64_t* offsets, int K, int p, int intercept, int rows_per_chunk,
-                      Plan& pl, double frac = 1.0, int64_t min_rows = 0,
-                      int family = FAMILY_LOGISTIC) {
+                      Plan& pl, double frac = 1.0, int64_t min_rows = 0) {
   pl.P = p + (intercept ? 1 : 0);
   pl.NT = (pl.P + 15) / 16;
   pl.T = pl.NT * (pl.NT + 1) / 2;
@@ -159,8 +126,7 @@ static bool make_plan(const int64_t* offsets, int K, int p, int intercept, int r
   // fused pass: chunk size from all rows (a warm-start level keeps the full
   // pass's chunk size: fewer, equally long chunks -- measured as fast)
   const int64_t n_total = offsets[K];
-  const int rpc =
-      rows_per_chunk > 0 ? rows_per_chunk : auto_rows_per_chunk(n_total, pl.NT, family);
+  const int rpc = rows_per_chunk > 0 ? rows_per_chunk : auto_rows_per_chunk(n_total);
   pl.part_chunk_begin.assign(K + 1, 0);
   pl.chunk_row0.clear();
   pl.chunk_rows.clear();
@@ -255,13 +221,23 @@ struct WideLayout {
   int64_t off_offsets, off_w, off_slabg, off_slabll, off_slabG, off_H;
   int64_t off_phase, off_bt, off_llprev, off_thprev, off_dprev, off_counters;
   int64_t total;
+  int64_t cap_rows, cap_gram;  // row-chunk / Gram-row-group capacity of the tables and slabs
 };
 
-static WideLayout make_wide_layout(const WidePlans& wp, int K, int64_t n_total, int P) {
+// Sized for the largest chunk counts over ALL level plans: a warm-start
+// level's row groups are sized from its own (smaller) row count, so with
+// uneven partitions it can have more row chunks / Gram row groups than the
+// final plan (e.g. P = 512, n_k = [1e7, 1e5, 1e5]: 258 vs 257 Gram groups).
+static WideLayout make_wide_layout(const std::vector<WidePlans>& plans, int K, int64_t n_total,
+                                   int P) {
   const int NB = (P + kWideTile - 1) / kWideTile;
   const int64_t PP = (int64_t)kWideTile * NB;
   const int64_t TB = NB * (NB + 1) / 2;
-  const int64_t nr = std::max(wp.rows.n_chunks, 1), ng = std::max(wp.gram.n_chunks, 1);
+  int64_t nr = 1, ng = 1;
+  for (const WidePlans& wp : plans) {
+    nr = std::max<int64_t>(nr, wp.rows.n_chunks);
+    ng = std::max<int64_t>(ng, wp.gram.n_chunks);
+  }
   WideLayout L;
   int64_t o = 0;
   auto take = [&](int64_t bytes) {
@@ -290,7 +266,32 @@ static WideLayout make_wide_layout(const WidePlans& wp, int K, int64_t n_total, 
   L.off_dprev = take(8LL * K * P);
   L.off_counters = take(16);
   L.total = o;
+  L.cap_rows = nr;
+  L.cap_gram = ng;
   return L;
+}
+
+// The wide path's plans: the warm-start levels (logistic, warm_start) then
+// all rows.  A level that would stream more than half of the rows is
+// skipped (it would cost more than the full passes it saves).
+static std::vector<WidePlans> wide_level_plans(const int64_t* offsets, int K, int p, int intercept,
+                                               int rows_per_chunk, bool levels) {
+  std::vector<WidePlans> plans;
+  const int P = p + (intercept ? 1 : 0);
+  if (levels) {
+    const int64_t min_rows = std::max<int64_t>(2048, 64LL * P);
+    for (double frac : warm_level_fracs(false)) {
+      WidePlans q;
+      make_wide_plans(offsets, K, p, intercept, rows_per_chunk, q, frac, min_rows);
+      int64_t rows = 0;
+      for (int c = 0; c < q.rows.n_chunks; ++c) rows += q.rows.chunk_rows[c];
+      if (rows <= offsets[K] / 2 && q.rows.n_chunks > 0) plans.push_back(std::move(q));
+    }
+  }
+  WidePlans fin;
+  make_wide_plans(offsets, K, p, intercept, rows_per_chunk, fin);
+  plans.push_back(std::move(fin));
+  return plans;
 }
 
 static int check_offsets(const int64_t* offsets, int K) {
@@ -340,11 +341,10 @@ int64_t dlsa_logistic_workspace_bytes(const int64_t* offsets, int32_t K, int32_t
                                       int32_t fit_intercept, int32_t rows_per_chunk) {
   if (check_offsets(offsets, K) != DLSA_OK) return -1;
   const int P = p + (fit_intercept ? 1 : 0);
-  if (P > DLSA_MAX_P_FUSED) {
-    WidePlans wp;
-    make_wide_plans(offsets, K, p, fit_intercept, rows_per_chunk, wp);
-    return make_wide_layout(wp, K, offsets[K], P).total;
-  }
+  if (P > DLSA_MAX_P_FUSED)  // sized for the warm-start levels too (an upper bound)
+    return make_wide_layout(wide_level_plans(offsets, K, p, fit_intercept, rows_per_chunk, true),
+                            K, offsets[K], P)
+        .total;
   Plan pl;
   make_plan(offsets, K, p, fit_intercept, rows_per_chunk, pl);
   return make_layout(pl, K).total;
@@ -460,10 +460,11 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
   const int P = p + (fit_intercept ? 1 : 0);
   const int NB = (P + kWideTile - 1) / kWideTile;
   const int64_t n_total = offsets[K];
-  WidePlans fin;
-  make_wide_plans(offsets, K, p, fit_intercept, opt.rows_per_chunk, fin);
-  const WideLayout L = make_wide_layout(fin, K, n_total, P);
-  g_stats.n_chunks = fin.gram.n_chunks;
+  const std::vector<WidePlans> plans = wide_level_plans(
+      offsets, K, p, fit_intercept, opt.rows_per_chunk,
+      family == FAMILY_LOGISTIC && opt.warm_start);
+  const WideLayout L = make_wide_layout(plans, K, n_total, P);
+  g_stats.n_chunks = plans.back().gram.n_chunks;
 
   char* ws = (char*)opt.workspace;
   bool owned = false;
@@ -535,19 +536,6 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
   };
   DLSA_HIP_TRY(hipMemcpyAsync(d_offsets, offsets, 8LL * (K + 1), hipMemcpyHostToDevice, stream));
 
-  std::vector<WidePlans> plans;
-  if (family == FAMILY_LOGISTIC && opt.warm_start) {
-    const int64_t min_rows = std::max<int64_t>(2048, 64LL * P);
-    for (double frac : warm_level_fracs(false)) {
-      WidePlans q;
-      make_wide_plans(offsets, K, p, fit_intercept, opt.rows_per_chunk, q, frac, min_rows);
-      int64_t rows = 0;
-      for (int c = 0; c < q.rows.n_chunks; ++c) rows += q.rows.chunk_rows[c];
-      if (rows <= n_total / 2 && q.rows.n_chunks > 0) plans.push_back(std::move(q));
-    }
-  }
-  plans.push_back(fin);
-
   // MIXED / MIXED_F32: bf16-MFMA Gram passes until the step is below
   // switch_tol, then fp64 Gram passes (the fused path's phase machine)
   const int start_phase =
@@ -593,6 +581,10 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
   for (size_t lvl = 0; lvl < plans.size(); ++lvl) {
     const WidePlans& q = plans[lvl];
     const bool final_level = lvl + 1 == plans.size();
+    if (q.rows.n_chunks > L.cap_rows || q.gram.n_chunks > L.cap_gram) {
+      set_error("internal: wide plan exceeds its workspace layout");
+      return DLSA_E_INVALID;
+    }
     DLSA_HIP_TRY(upload_plan(q.rows, L.off_r_row0, L.off_r_rows, L.off_r_part, d_rcb));
     DLSA_HIP_TRY(upload_plan(q.gram, L.off_g_row0, L.off_g_rows, L.off_g_part, d_gcb));
     wa.n_gchunks = q.gram.n_chunks;
@@ -612,7 +604,10 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
     sa.subsample = final_level ? 0 : 1;
     sa.level_tol = warm_level_tol(false);
     sa.switch_tol = final_level ? opt.switch_tol : 0.0;
-    const int it_end = final_level ? max_iter : std::min(max_iter, it + 10);
+    // a warm-start level has its own budget of kLevelIters iterations; the
+    // full-data level always gets max_iter (so a small max_iter still ends
+    // with full-row passes and a published Sig_inv)
+    const int it_end = it + (final_level ? max_iter : kLevelIters);
     for (; it < it_end && (n_running[0] + n_running[1]) > 0 && q.rows.n_chunks > 0; ++it) {
       DLSA_HIP_TRY(timed(&g_stats.ms_wide_row, [&] {
         return launch_wide_row(wa, standardize, family, q.rows.n_chunks, stream);
@@ -704,7 +699,7 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
                     theta, sig_inv, sig_inv_theta, loglik, iters, status, opt, stream, t_start);
 
   Plan pl;
-  make_plan(offsets, K, p, fit_intercept, opt.rows_per_chunk, pl, 1.0, 0, family);
+  make_plan(offsets, K, p, fit_intercept, opt.rows_per_chunk, pl);
   const Layout L = make_layout(pl, K);
   g_stats.n_chunks = pl.n_chunks;
 
@@ -807,13 +802,17 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
   pa.p = p;
   pa.P = P;
   pa.intercept = fit_intercept ? 1 : 0;
-  const bool perwave = use_perwave_pass();
-  if (perwave && pl.NT > 8) {
-    set_error("DLSA_PASS=perwave handles P <= 128 only");
-    return DLSA_E_UNSUPPORTED;
-  }
-  pa.slot_bytes = perwave ? pass_slot_bytes(pl.NT) : coop_slot_bytes(pl.NT, p);
   const int approx_prec = opt.hessian_mode == DLSA_HESSIAN_MIXED_F32 ? PREC_F32 : PREC_BF16;
+  // cooperative-pass LDS ring: two workgroups per CU (P <= 112) so that one's
+  // row phase and barrier waits overlap the other's tile phase (measured
+  // 27.4 -> 21.8 ms per bf16 pass at config 2 against one workgroup with a
+  // deeper ring)
+  pa.slot_bytes = coop_slot_bytes(pl.NT, p);
+  {
+    const int wg_per_cu = pl.NT < 8 ? 2 : 1;
+    const int budget = 160 * 1024 / wg_per_cu - coop_extra_bytes(pl.NT);
+    pa.nslot = std::max(2, std::min(budget / pa.slot_bytes, 6));
+  }
 
   SolveArgs sa;
   memset(&sa, 0, sizeof(sa));
@@ -876,48 +875,17 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
     // a 0.2-relative step (warm_level_tol)
     sa.level_tol = warm_level_tol(true);
     sa.switch_tol = final_level ? opt.switch_tol : 0.0;
-    const int it_end = final_level ? max_iter : std::min(max_iter, it + 10);
+    const int it_end = it + (final_level ? max_iter : kLevelIters);  // see fit_wide
   for (; it < it_end && (n_running[0] + n_running[1]) > 0 && q.n_chunks > 0; ++it) {
     for (int ph = 0; ph < 2; ++ph) {
       if (n_running[ph] == 0) continue;
       const bool f64 = ph == PHASE_F64;
       pa.want_phase = ph;
-      const bool reg = use_reg_pass(q.NT, f64, family);
-      const bool ws = f64 && !reg && use_ws_pass(q.NT);
-      const bool lite =
-          !f64 && !reg && family == FAMILY_LOGISTIC && use_lite_pass(q.NT, p, approx_prec);
-      int nslot;
-      if (lite) {
-        nslot = lite_nslot(q.NT, p);
-      } else if (ws) {
-        nslot = ws_nslot(q.NT, p);
-      } else if (perwave) {
-        int waves = pass_waves_per_cu(f64);
-        if (const char* e = getenv(f64 ? "DLSA_WAVES_F64" : "DLSA_WAVES_F32")) waves = atoi(e);
-        nslot = (160 * 1024 / std::max(waves, 1)) / pa.slot_bytes;
-        nslot = std::max(2, std::min(nslot, 4));
-      } else {
-        // two workgroups per CU (P <= 112): one's row phase and barrier waits
-        // overlap the other's tile phase (measured 27.4 -> 21.8 ms per bf16
-        // pass at config 2 against one workgroup with a deeper ring)
-        int wg_per_cu = pl.NT < 8 ? 2 : 1;
-        if (const char* e = getenv(f64 ? "DLSA_WG_F64" : "DLSA_WG_LOWP")) wg_per_cu = atoi(e);
-        const int budget =
-            160 * 1024 / std::max(wg_per_cu, 1) - coop_extra_bytes(pl.NT);
-        nslot = std::max(2, std::min(budget / pa.slot_bytes, 6));
-      }
-      if (const char* e = getenv("DLSA_NSLOT"))
-        if (!lite) nslot = std::max(ws ? 3 : 2, std::min(atoi(e), perwave ? 4 : (ws ? 5 : 6)));
-      pa.nslot = nslot;
-      pa.slot_bytes = lite ? lite_slot_bytes(q.NT, p)
-                           : ws ? ws_slot_bytes(q.NT, p)
-                                : (perwave ? pass_slot_bytes(q.NT) : coop_slot_bytes(q.NT, p));
+      // exact (fp64 Hessian) passes: the per-wave kernel up to P = 128, the
+      // cooperative one above; approximate passes: the cooperative kernel
+      const bool wave = f64 && q.NT <= kWaveMaxNT;
       DLSA_HIP_TRY(timed(f64 ? &g_stats.ms_pass_fp64 : &g_stats.ms_pass_fp32, [&] {
-        if (reg) return launch_irls_reg(pa, q.NT, f64, standardize, family, q.n_chunks, stream);
-        if (ws) return launch_irls_ws(pa, q.NT, standardize, family, q.n_chunks, stream);
-        if (lite) return launch_irls_lite(pa, q.NT, standardize, q.n_chunks, stream);
-        if (perwave)
-          return launch_irls_pass(pa, q.NT, f64, standardize, family, q.n_chunks, stream);
+        if (wave) return launch_irls_wave(pa, q.NT, standardize, family, q.n_chunks, stream);
         return launch_irls_coop(pa, q.NT, f64 ? PREC_F64 : approx_prec, standardize, family,
                                 q.n_chunks, stream);
       }));
@@ -1244,7 +1212,7 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
     sa.subsample = final_level ? 0 : 1;
     sa.level_tol = warm_level_tol(true);
     sa.switch_tol = 0.0;
-    const int it_end = final_level ? max_iter : std::min(max_iter, it + 10);
+    const int it_end = it + (final_level ? max_iter : kLevelIters);  // see fit_wide
     for (; it < it_end && n_running > 0 && qn.n_chunks > 0; ++it) {
       DLSA_HIP_TRY(timed(&g_stats.ms_pass_fp64,
                          [&] { return launch_cat_pass(ca, standardize, qn.n_chunks, stream); }));

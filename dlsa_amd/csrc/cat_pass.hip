@@ -345,14 +345,9 @@ __global__ __launch_bounds__(256) void cat_mark_kernel(const CatArgs a, const in
 template <int QN, int FM, int NTHR, bool STD>
 static hipError_t launch_cat_t(const CatArgs& a, int n_chunks, size_t lds, hipStream_t s) {
   auto kern = cat_pass_kernel<QN, FM, NTHR, STD>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    // dynamic + the kernel's static tables <= 160 KB
-    hipError_t e = hipFuncSetAttribute((const void*)kern,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       160 * 1024 - kCatStaticLds);
+  {
+    hipError_t e = ensure_max_lds((const void*)kern, 160 * 1024 - kCatStaticLds);
     if (e != hipSuccess) return e;
-    attr_set = true;
   }
   hipLaunchKernelGGL(kern, dim3(n_chunks), dim3(NTHR), lds, s, a);
   return hipGetLastError();

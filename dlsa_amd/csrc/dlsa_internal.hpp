@@ -18,15 +18,12 @@ enum : int32_t { PHASE_F32 = 0, PHASE_F64 = 1, PHASE_DONE = 2, PHASE_LEVEL_DONE 
 enum : int32_t { STATUS_RUNNING = -1 };
 enum : int32_t { FAMILY_LOGISTIC = 0, FAMILY_GAUSSIAN = 1 };
 
-// Rows of X one wave stages per LDS slot (4 MFMA k-steps of 4 rows).
-constexpr int kRowsPerBlock = 8;
-// Cooperative pass: 4 waves per workgroup, 32-row blocks.
-constexpr int kCoopWaves = 4;
+// Cooperative pass: 4 (8) waves per workgroup, 32-row blocks.
 constexpr int kCoopRows = 32;
 // MFMA arithmetic of a pass's Hessian.
 enum : int32_t { PREC_BF16 = 0, PREC_F32 = 1, PREC_F64 = 2 };
 
-// Arguments of the fused IRLS pass (one wave = one chunk of one partition).
+// Arguments of the fused IRLS pass (one workgroup = one chunk of one partition).
 struct PassArgs {
   const double* X;            // [n_total, p]
   const double* y;            // [n_total]
@@ -46,7 +43,7 @@ struct PassArgs {
   int32_t P;                  // p + intercept
   int32_t intercept;
   int32_t want_phase;
-  int32_t nslot;              // LDS ring depth (slots of kRowsPerBlock rows)
+  int32_t nslot;              // cooperative pass: LDS ring depth (32-row slots)
   int32_t slot_bytes;
 };
 
@@ -187,29 +184,15 @@ hipError_t launch_loglik_eval(const EvalArgs& a, int n_chunks, hipStream_t s);
 hipError_t launch_loglik_reduce(const double* partial, const int32_t* pcb, int K, int B,
                                 double* out, hipStream_t s);
 int eval_slot_bytes(int p);
-hipError_t launch_irls_reg(const PassArgs& a, int NT, bool f64, bool standardize, int family,
-                           int n_chunks, hipStream_t s);
-constexpr int kRegMaxNT = 7;
-// wave-specialised fp64 pass (irls_ws_impl.hpp): P <= 128
-hipError_t launch_irls_ws(const PassArgs& a, int NT, bool standardize, int family, int n_chunks,
-                          hipStream_t s);
-int ws_slot_bytes(int NT, int p);  // one producer sub-slot
-int ws_nslot(int NT, int p);
-constexpr int kWsMaxNT = 8;
-// light-weight approximate-Hessian (bf16) pass (irls_lite_impl.hpp): P <= 112, P <~ 2p
-hipError_t launch_irls_lite(const PassArgs& a, int NT, bool standardize, int n_chunks,
+// per-wave fp64 pass (irls_wave_impl.hpp): P <= 128
+hipError_t launch_irls_wave(const PassArgs& a, int NT, bool standardize, int family, int n_chunks,
                             hipStream_t s);
-bool lite_fits(int NT, int p);
-int lite_slot_bytes(int NT, int p);
-int lite_nslot(int NT, int p);  // register-streaming pass: fp64 accumulators of all tiles in one wave
-hipError_t launch_irls_pass(const PassArgs& a, int NT, bool f64, bool standardize,
-                            int family, int n_chunks, hipStream_t s);
-int pass_slot_bytes(int NT);
+int wave_lds_bytes(int NT, int p);
+constexpr int kWaveMaxNT = 8;
 hipError_t launch_irls_coop(const PassArgs& a, int NT, int prec, bool standardize, int family,
                             int n_chunks, hipStream_t s);
 int coop_slot_bytes(int NT, int p);
 int coop_extra_bytes(int NT);  // LDS beyond the ring
-int pass_waves_per_cu(bool f64);
 hipError_t launch_newton_solve(const SolveArgs& a, int K, hipStream_t s);
 hipError_t launch_fit_init(const int64_t* offsets_dev, int K, int P, int start_phase,
                            double* theta, int32_t* phase, int32_t* backtracks,
@@ -227,5 +210,9 @@ hipError_t launch_simulate(double* X, double* y, int64_t n, int p, uint64_t seed
                            int64_t row0, hipStream_t s);
 
 void set_error(const std::string& msg);
+
+// Raise a kernel's dynamic-LDS limit to `bytes` once per (kernel, device):
+// thread-safe (one process may drive several GPUs from several threads).
+hipError_t ensure_max_lds(const void* kernel, int bytes);
 
 }  // namespace dlsa

@@ -172,12 +172,9 @@ hipError_t launch_loglik_eval(const EvalArgs& a, int n_chunks, hipStream_t s) {
   const int PM = ((a.P + 7) / 8) * 8;
   const size_t lds = (size_t)a.nslot * a.slot_bytes +
                      ((size_t)a.nbeta * PM + 2 * PM + EW * EMAXB) * sizeof(double);
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)loglik_eval_kernel,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  {
+    hipError_t e = ensure_max_lds((const void*)loglik_eval_kernel, 160 * 1024);
     if (e != hipSuccess) return e;
-    attr_set = true;
   }
   hipLaunchKernelGGL(loglik_eval_kernel, dim3(n_chunks), dim3(256), lds, s, a);
   return hipGetLastError();

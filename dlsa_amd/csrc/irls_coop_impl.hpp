@@ -71,6 +71,28 @@ __device__ __forceinline__ void wait_vmcnt_le(int n) {
   }
 }
 
+// Workgroup barrier for the block loop: this wave's LDS reads/writes are
+// complete (lgkmcnt(0)), then s_barrier.  Unlike __syncthreads() it carries no
+// memory fence, whose lowering drains vmcnt to 0 -- that would wait for the
+// LDS-DMA of the blocks still streaming in, i.e. empty the ring at every
+// barrier.  The "memory" clobber keeps the compiler from moving LDS accesses
+// across it; the DMA'd slot of a block is waited for by each wave's counted
+// vmcnt before the first barrier that publishes it.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Buffer resource with every word wave-uniform (readfirstlane): the LDS-DMA
+// loads then take it in SGPRs instead of a waterfall loop per load.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(uintptr_t base, uintptr_t bytes) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)base >> 32));
+  const uint32_t nr = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(bytes < 0x7FFFFFF0u ? bytes : 0x7FFFFFF0u));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, (int)nr,
+                                           0x00020000);
+}
+
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double v) {
   const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
@@ -159,12 +181,7 @@ __host__ __device__ __forceinline__ int npieces_for(int p) { return (RB * p * 8 
 
 // Waves per workgroup: 4 for P <= 128 (8 lanes per row in the row phase),
 // 8 above (16 lanes per row keeps the per-lane feature count <= 12).
-// DLSA_COOP_W=8 selects 8 waves for small P too (profiling knob).
-inline int coop_waves(int NT) {
-  if (NT > 8) return 8;
-  if (const char* e = getenv("DLSA_COOP_W")) return atoi(e) == 8 ? 8 : 4;
-  return 4;
-}
+constexpr int coop_waves(int NT) { return NT > 8 ? 8 : 4; }
 
 // A slot holds exactly the block's pieces: a wave's surplus issues (the piece
 // count is rounded up to the wave count so that every wave waits on the same
@@ -273,15 +290,17 @@ void irls_coop_kernel(const PassArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int chunk = blockIdx.x;
-  const int part = a.chunk_part[chunk];
+  const int part = __builtin_amdgcn_readfirstlane(a.chunk_part[chunk]);
   if (a.phase[part] != a.want_phase) return;  // workgroup-uniform
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int p = a.p, P = a.P, ic = a.intercept;
-  const int64_t row0 = a.chunk_row0[chunk];
-  const int nrows = a.chunk_rows[chunk];
+  const int64_t row0 =
+      ((int64_t)__builtin_amdgcn_readfirstlane((int)(a.chunk_row0[chunk] >> 32)) << 32) |
+      (uint32_t)__builtin_amdgcn_readfirstlane((int)a.chunk_row0[chunk]);
+  const int nrows = __builtin_amdgcn_readfirstlane(a.chunk_rows[chunk]);
   const int nb = (nrows + RB - 1) / RB;
   const int nslot = a.nslot;
   const int slot_bytes = a.slot_bytes;
@@ -306,6 +325,11 @@ void irls_coop_kernel(const PassArgs a) {
     beta[m] = (f < P) ? a.theta[(int64_t)part * P + f] : 0.0;
     gacc[m] = 0.0;
   }
+  // re-define beta by an opaque instruction so its loads are waited for here,
+  // once: otherwise the compiler's loop-carried wait for them sits inside the
+  // block loop as vmcnt(1) and drains the ring
+#pragma unroll
+  for (int m = 0; m < M; ++m) asm volatile("" : "+v"(beta[m]));
   double llacc = 0.0;
   int tI[G::TPW], tJ[G::TPW];  // this wave's tiles (bf16 path)
 #pragma unroll
@@ -339,17 +363,15 @@ void irls_coop_kernel(const PassArgs a) {
   // 64-bit address arithmetic.
   const uintptr_t xcb = (uintptr_t)(a.X + row0 * p) & ~(uintptr_t)15;
   const uintptr_t xend = a.x_last16 + 16;
-  const __amdgpu_buffer_rsrc_t xr_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)xcb, (short)0, (int)min<uintptr_t>(xend - xcb, 0x7FFFFFF0u), 0x00020000);
+  const __amdgpu_buffer_rsrc_t xr_rsrc = uniform_rsrc(xcb, xend - xcb);
   const uintptr_t ycb = (uintptr_t)(a.y + row0);
-  const __amdgpu_buffer_rsrc_t yr_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)ycb, (short)0, (int)min<uintptr_t>(a.y_last4 + 4 - ycb, 0x7FFFFFF0u), 0x00020000);
+  const __amdgpu_buffer_rsrc_t yr_rsrc = uniform_rsrc(ycb, a.y_last4 + 4 - ycb);
   const int vx = lane * 16, vy = lane * 4;
   auto issue = [&](int blk) {
     const int bb = blk < nb ? blk : nb - 1;  // tail: harmless re-fetch, fixed counts
     char* sbase = smem + (blk % nslot) * slot_bytes;
     const uintptr_t start = (uintptr_t)(a.X + (row0 + (int64_t)bb * RB) * p);
-    const int so = (int)((start & ~(uintptr_t)15) - xcb);
+    const int so = __builtin_amdgcn_readfirstlane((int)((start & ~(uintptr_t)15) - xcb));
     for (int i = 0; i < d; ++i) {
       int j = wid + W * i;
       const int jj = j < npieces ? j : npieces - 1;
@@ -365,7 +387,7 @@ void irls_coop_kernel(const PassArgs a) {
 
   for (int b = 0; b < nb; ++b) {
     wait_vmcnt_le<MAXW>(keep);  // this wave's pieces of block b landed
-    __syncthreads();            // B1: everyone's pieces landed, block b-1 fully consumed
+    lds_barrier();              // B1: everyone's pieces landed, block b-1 fully consumed
     issue(b + nslot - 1);
 
     const char* slot = smem + (b % nslot) * slot_bytes;
@@ -445,7 +467,7 @@ void irls_coop_kernel(const PassArgs a) {
         }
       }
     }
-    __syncthreads();  // B2: w, r of all 32 rows visible
+    lds_barrier();  // B2: w, r (and the bf16 operand images) of all 32 rows visible
 
     // ---- C: tile phase -----------------------------------------------------
     if constexpr (DLSA_ABLATE != 1 && DLSA_ABLATE != 3) {
@@ -512,13 +534,8 @@ static hipError_t launch_c(const PassArgs& a, int n_chunks, hipStream_t s) {
   auto kern = irls_coop_kernel<NT, W, PREC, STD, FAM>;
   const size_t lds =
       (size_t)a.nslot * a.slot_bytes + coop_extra_bytes_impl(NT);
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)kern,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
+  hipError_t e = ensure_max_lds((const void*)kern, 160 * 1024);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3(n_chunks), dim3(64 * W), lds, s, a);
   return hipGetLastError();
 }
@@ -547,10 +564,7 @@ static hipError_t launch_coop_ntw(const PassArgs& a, int prec, bool std_, int fa
 template <int NT>
 static hipError_t launch_coop_nt(const PassArgs& a, int prec, bool std_, int family,
                                  int n_chunks, hipStream_t s) {
-  if constexpr (NT <= 8) {
-    if (coop_waves(NT) == 4) return launch_coop_ntw<NT, 4>(a, prec, std_, family, n_chunks, s);
-  }
-  return launch_coop_ntw<NT, 8>(a, prec, std_, family, n_chunks, s);
+  return launch_coop_ntw<NT, coop_waves(NT)>(a, prec, std_, family, n_chunks, s);
 }
 
 }  // namespace dlsa

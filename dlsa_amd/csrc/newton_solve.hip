@@ -388,6 +388,12 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
   }
   dm = block_max(dm, red);
   tm = block_max(tm, red);
+  if (!isfinite(dm) && !a.subsample) {
+    // keep the last finite iterate (each thread restores the entries it
+    // wrote): the status reports the failure and the combine step excludes
+    // the partition
+    for (int f = tid; f < P; f += 256) th[f] = tp[f];
+  }
   if (a.family == FAMILY_GAUSSIAN) {
     // OLS: theta was 0, one Newton step is the closed form (X^T X)^-1 X^T y;
     // residual sum of squares = y^T y - theta^T X^T y = -2 ll(0) - theta . g
@@ -490,12 +496,9 @@ __global__ __launch_bounds__(256) void partials_sum_kernel(const SolveArgs a, in
 
 template <int NT>
 static hipError_t launch_solve_t(const SolveArgs& a, int K, size_t lds, hipStream_t s) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)newton_solve_kernel<NT>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  {
+    hipError_t e = ensure_max_lds((const void*)newton_solve_kernel<NT>, 160 * 1024);
     if (e != hipSuccess) return e;
-    attr_set = true;
   }
   constexpr int T = NT * (NT + 1) / 2;
   hipLaunchKernelGGL(partials_sum_kernel, dim3((T + 1 + 3) / 4, K), dim3(256), 0, s, a, T, 16 * NT);

@@ -210,12 +210,9 @@ hipError_t launch_partition_scatter(const int32_t* pid, int64_t n, int K, int64_
     arr.dst[a] = (char*)dst[a];
     arr.row_bytes[a] = row_bytes[a];
   }
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)part_scatter_kernel,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  {
+    hipError_t e = ensure_max_lds((const void*)part_scatter_kernel, 160 * 1024);
     if (e != hipSuccess) return e;
-    attr_set = true;
   }
   const size_t lds = (size_t)kPartSubRows * 8 + (size_t)K * 8;
   hipLaunchKernelGGL(part_scatter_kernel, dim3(nb), dim3(kScatterThreads), lds, s, pid, n, K, rows_per_block,

@@ -617,13 +617,10 @@ __global__ __launch_bounds__(512, 1) void wide_gram_all_bf16_kernel(const WideAr
 template <bool STD, int NT16>
 static hipError_t launch_gram_all_t(const WideArgs& a, hipStream_t s) {
   auto kern = wide_gram_all_bf16_kernel<STD, NT16>;
-  static bool attr_set = false;
   const int lds = 2 * 16 * NT16 * ZS;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)kern,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  {
+    hipError_t e = ensure_max_lds((const void*)kern, lds);
     if (e != hipSuccess) return e;
-    attr_set = true;
   }
   const int grid = ((a.n_gchunks + 7) / 8) * 8 * zall_groups(NT16);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, s, a);
@@ -950,6 +947,8 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
     // OLS: rss = y^T y - theta^T X^T y = -2 ll(0) - theta . g
     a.loglik[k] = -2.0 * ll - tg;
     a.status[k] = isfinite(dm) ? DLSA_STATUS_OK : DLSA_STATUS_NONFINITE;
+    if (!isfinite(dm))
+      for (int f = 0; f < P; ++f) th[f] = tp[f];
     a.phase[k] = PHASE_DONE;
     return;
   }
@@ -967,6 +966,9 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
     return;
   }
   if (!isfinite(dm)) {
+    // keep the last finite iterate: the status reports the failure, and the
+    // combine step excludes the partition (dlsa.py reduce)
+    for (int f = 0; f < P; ++f) th[f] = tp[f];
     a.status[k] = DLSA_STATUS_NONFINITE;
     return;
   }
@@ -1043,12 +1045,9 @@ hipError_t launch_wide_assemble(const WideArgs& a, const int32_t* gcb, double* H
 
 hipError_t launch_wide_newton(const SolveArgs& sa, const WideArgs& wa, const int32_t* rcb,
                               double* Hfull, int K, hipStream_t s) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)wide_newton_kernel,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  {
+    hipError_t e = ensure_max_lds((const void*)wide_newton_kernel, 160 * 1024);
     if (e != hipSuccess) return e;
-    attr_set = true;
   }
   hipLaunchKernelGGL(wide_newton_kernel, dim3(K), dim3(1024), wide_newton_lds_bytes(wa.NB), s,
                      sa, wa, rcb, Hfull);

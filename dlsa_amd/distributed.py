@@ -7,7 +7,8 @@ partitions in HBM, pre-reduces them on the device into
 ``[sum Sig_inv | sum Sig_inv theta | sum theta | K]`` (P^2 + 2P + 1 fp64,
 81.6 KB at P = 100) and ONE ``all_reduce(SUM)`` over RCCL/xGMI combines the
 ranks.  Every rank then holds the global sums and can solve the WLSE and run
-the LARS/DBIC path locally (dlsa/dlsa.py:44-52, :70-100).
+the LARS/DBIC path locally (dlsa/dlsa.py:44-52, :70-100).  The global row
+count N (for the DBIC) rides in the same buffer: one collective in all.
 """
 
 from __future__ import annotations
@@ -51,15 +52,27 @@ def finish(S, v, sum_theta, K, n_global, fit_intercept=False, lars_type="lasso")
             "dbic_support": support, "path": path, "Sig_inv_sum": S}
 
 
-def dlsa_fit_sharded(X, y, offsets, n_global=None, fit_intercept=False, lars_type="lasso",
+def combine_and_finish(buf, P, fit_intercept=False, lars_type="lasso", group=None):
+    """The exchange step and the host tail of the sharded path: ONE
+    all-reduce of this rank's ``[sum Sig_inv | sum Sig_inv theta | sum theta |
+    K | N]`` buffer (P^2 + 2P + 2 fp64, the layout of
+    ``reduce_partitions_device(fit, n_rows=True)``), then WLSE / ONESHOT /
+    LARS / DBIC from the global sums on every rank."""
+    combine(buf, group)
+    b = buf.cpu().numpy() if hasattr(buf, "cpu") else np.asarray(buf)
+    S, v, st, K = split_reduced(b[:-1], P)
+    return finish(S, v, st, K, int(round(float(b[-1]))), fit_intercept, lars_type)
+
+
+def dlsa_fit_sharded(X, y, offsets, fit_intercept=False, lars_type="lasso",
                      group=None, codes=None, levels=None, **fit_kw):
     """Fit this rank's partitions on its GPU and return the global DLSA result.
 
     X, y, offsets describe the LOCAL shard (rows already on this rank's
     device).  With ``codes``/``levels`` X holds the numeric columns of the
-    categorical-code layout (``logistic_model_batched_categorical``).
-    ``n_global`` (total rows over all ranks, for DBIC) defaults to the
-    all-reduced row count.
+    categorical-code layout (``logistic_model_batched_categorical``).  The
+    row count N of the DBIC is summed in the same single collective as the
+    partition sums (reference: the shuffle + collect of dlsa/dlsa.py:30-34).
     """
     from .models import logistic_model_batched, logistic_model_batched_categorical
 
@@ -68,16 +81,7 @@ def dlsa_fit_sharded(X, y, offsets, n_global=None, fit_intercept=False, lars_typ
                                                  fit_intercept=fit_intercept, **fit_kw)
     else:
         fit = logistic_model_batched(X, y, offsets, fit_intercept=fit_intercept, **fit_kw)
-    buf = reduce_partitions_device(fit)
-    combine(buf, group)
-    S, v, st, K = split_reduced(buf.cpu().numpy(), fit.P)
-    if n_global is None:
-        import torch
-
-        import torch.distributed as dist
-        nt = torch.tensor([float(fit.n_rows)], dtype=torch.float64, device=buf.device)
-        combine(nt, group)
-        n_global = int(nt.item())
-    out = finish(S, v, st, K, n_global, fit_intercept, lars_type)
+    buf = reduce_partitions_device(fit, n_rows=True)
+    out = combine_and_finish(buf, fit.P, fit_intercept, lars_type, group)
     out["fit"] = fit
     return out

@@ -52,20 +52,51 @@ def _frame(S, v, sum_theta, K, columns):
                         columns=["beta_byOLS", "beta_byONESHOT"] + list(columns))
 
 
-def reduce_partitions_device(fit):
+#: statuses whose outputs are not usable estimates: their Sig_inv / theta are
+#: replaced by the reference's zero frame (models.py:84-91) in the reduce
+EXCLUDED_STATUS = {2: "singular", 4: "nonfinite"}
+
+
+def reduce_partitions_device(fit, n_rows=False):
     """[sum Sig_inv | sum Sig_inv theta | sum theta | K] of a BatchedFit, as a
-    device tensor of P*P + 2P + 1 fp64 (the buffer the RCCL all-reduce sums)."""
+    device tensor of P*P + 2P + 1 fp64 (the buffer the RCCL all-reduce sums);
+    with ``n_rows`` one more entry holds the fitted row count, so the sharded
+    path's single collective also carries N for the DBIC.
+
+    Partitions whose status is singular or nonfinite are summed as the
+    reference's all-zero frame (models.py:84-91) with a warning naming them:
+    the reference's sklearn fit would not have produced a usable estimate
+    either, and one NaN block would otherwise turn WLSE, ONESHOT and the
+    LARS/DBIC path into NaN.  Empty / missing-level partitions already are
+    zero frames."""
+    import warnings
+
     import torch
 
     P, K = fit.P, fit.K
-    out = torch.empty((P * P + 2 * P + 1,), dtype=torch.float64, device=fit.theta.device)
+    sig, sigt, th = fit.sig_inv, fit.sig_inv_theta, fit.theta
+    st = fit.status.cpu().numpy()
+    bad = np.nonzero(np.isin(st, list(EXCLUDED_STATUS)))[0]
+    if bad.size:
+        warnings.warn("partitions " + str(bad.tolist()) + " ended "
+                      + str(sorted({EXCLUDED_STATUS[int(v)] for v in st[bad]}))
+                      + ": summed as zero frames (excluded from WLSE / ONESHOT / DBIC)")
+        keep = torch.from_numpy(~np.isin(st, list(EXCLUDED_STATUS))).to(th.device)
+        zero = torch.zeros((), dtype=th.dtype, device=th.device)
+        sig = torch.where(keep[:, None, None], sig, zero).contiguous()
+        sigt = torch.where(keep[:, None], sigt, zero).contiguous()
+        th = torch.where(keep[:, None], th, zero).contiguous()
+    out = torch.empty((P * P + 2 * P + 1 + (1 if n_rows else 0),), dtype=torch.float64,
+                      device=th.device)
     lib = _hip.load()
-    stream = ctypes.c_void_p(torch.cuda.current_stream(fit.theta.device).cuda_stream)
-    rc = lib.dlsa_reduce_partitions(ctypes.c_void_p(fit.sig_inv.data_ptr()),
-                                    ctypes.c_void_p(fit.sig_inv_theta.data_ptr()),
-                                    ctypes.c_void_p(fit.theta.data_ptr()), K, P,
+    stream = ctypes.c_void_p(torch.cuda.current_stream(th.device).cuda_stream)
+    rc = lib.dlsa_reduce_partitions(ctypes.c_void_p(sig.data_ptr()),
+                                    ctypes.c_void_p(sigt.data_ptr()),
+                                    ctypes.c_void_p(th.data_ptr()), K, P,
                                     ctypes.c_void_p(out.data_ptr()), stream)
     _hip.check(rc, "dlsa_reduce_partitions")
+    if n_rows:
+        out[-1] = float(fit.n_rows)
     return out
 
 

@@ -150,31 +150,44 @@ def test_partition_offsets():
 
 # ---- multi-rank combine (gloo, world_size 2) -------------------------------
 
-def _gloo_worker(rank, world, port, golden_dir, q):
+def _gloo_worker(rank, world, port, golden_dir, q, shards):
     import torch
     import torch.distributed as dist
 
-    from dlsa_amd.distributed import combine, finish
-    from dlsa_amd.dlsa import split_reduced
+    from dlsa_amd.distributed import combine_and_finish
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     g = np.load(os.path.join(golden_dir, "config1_n1e5_p10_K4.npz"))
     outs = g["outs_noint"]
-    mine = outs[rank::world]  # partitions sharded over ranks
+    mine = outs[shards[rank]]  # this rank's partitions (25 000 rows each)
     P = outs.shape[1]
+    # the local buffer in the layout of reduce_partitions_device(fit, n_rows=True):
+    # [sum Sig_inv | sum Sig_inv theta | sum theta | K | N]
     buf = np.concatenate([mine[:, :, 3:].sum(0).ravel(), mine[:, :, 2].sum(0),
-                          mine[:, :, 1].sum(0), [float(len(mine))]])
-    t = torch.from_numpy(buf)
-    combine(t)
-    S, v, st, K = split_reduced(t.numpy(), P)
-    res = finish(S, v, st, K, 100000)
-    q.put((rank, res["wlse"], res["oneshot"], res["dbic_support"].tolist(), K))
+                          mine[:, :, 1].sum(0), [float(len(mine)), 25000.0 * len(mine)]])
+    calls = []
+    orig = dist.all_reduce
+
+    def counting(*a, **k):
+        calls.append(1)
+        return orig(*a, **k)
+
+    dist.all_reduce = counting
+    res = combine_and_finish(torch.from_numpy(buf), P)
+    dist.all_reduce = orig
+    q.put((rank, res["wlse"], res["oneshot"], res["dbic_support"].tolist(),
+           res["path"]["BIC"], len(calls)))
     dist.destroy_process_group()
 
 
-def test_distributed_combine_gloo(golden_dir):
+@pytest.mark.parametrize("shards", [([0, 2], [1, 3]), ([0, 1, 3], [2])])
+def test_distributed_combine_gloo(golden_dir, shards):
+    """The sharded path's exchange + host tail (distributed.combine_and_finish)
+    on world_size 2 with even and uneven shards: ONE all-reduce carries the
+    partition sums, K and N; every rank gets the golden WLSE / ONESHOT and the
+    DBIC path of the full data (n = 1e5)."""
     import multiprocessing as mp
     import socket
 
@@ -184,7 +197,8 @@ def test_distributed_combine_gloo(golden_dir):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_gloo_worker, args=(r, 2, port, golden_dir, q)) for r in range(2)]
+    ps = [ctx.Process(target=_gloo_worker, args=(r, 2, port, golden_dir, q, shards))
+          for r in range(2)]
     for p_ in ps:
         p_.start()
     res = [q.get(timeout=120) for _ in range(2)]
@@ -192,11 +206,14 @@ def test_distributed_combine_gloo(golden_dir):
         p_.join(timeout=60)
         assert p_.exitcode == 0
     g = np.load(os.path.join(golden_dir, "config1_n1e5_p10_K4.npz"))
-    for rank, wlse, oneshot, support, K in res:
-        assert K == 4
+    S = g["outs_noint"][:, :, 3:].sum(0)
+    ref = O.lars_lsa(S, g["wlse_noint"], False, 100000, type="lasso")
+    for rank, wlse, oneshot, support, bic, n_calls in res:
+        assert n_calls == 1
         assert np.abs(wlse - g["wlse_noint"]).max() < 1e-10
         assert np.abs(oneshot - g["oneshot_noint"]).max() < 1e-12
         assert support == [0, 1, 2, 3]
+        assert np.allclose(bic, ref["BIC"], rtol=1e-9, atol=1e-6)  # N = 1e5 reached the DBIC
 
 
 def test_dummy_design_generator():
