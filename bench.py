@@ -2,17 +2,21 @@
 """DLSA logistic fit benchmark (BASELINE.json metric, config 2 by default).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
+                    [--scaling weak|strong]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
 One step = one complete DLSA fit of the GPU's shard: batched Newton/IRLS over
 all partitions (approximate-Hessian passes + the final fp64 pass whose Hessian
-is Sig_inv), local partition reduction in HBM, one RCCL all-reduce of the
-P^2+2P+1 sums across ranks, WLSE solve, LARS path and DBIC selection on the
-host.  Data are synthetic, generated in HBM by the counter-based generator
-before the timed region.
+is Sig_inv), local partition reduction in HBM, ONE RCCL all-reduce of the
+P^2+2P+2 sums (Sig_inv, Sig_inv theta, theta, K, N) across ranks, WLSE solve,
+LARS path and DBIC selection on the host.  Data are synthetic, generated in
+HBM by the counter-based generator before the timed region.
 
-Configs (BASELINE.json "configs"); per GPU (weak scaling):
+Configs (BASELINE.json "configs"); sizes per GPU under weak
+scaling (the default), or of the whole job under --scaling strong (rank r
+then owns partitions [rK/N, (r+1)K/N) of the same global data set, SURVEY
+8(e)):
   2  logistic n = 1e8, p = 100, K = 1024            (default; the headline metric)
   3  logistic n = 1.5e7, p = 181 + intercept, K = 128 (airline-like dummy-coded design;
                                                      1.2e8 rows on 8 GPUs)
@@ -20,8 +24,9 @@ Configs (BASELINE.json "configs"); per GPU (weak scaling):
   4  OLS      n = 1.25e8, p = 64, K = 128           (1e9 rows / 1024 partitions on 8 GPUs)
 
 Rank 0 prints one JSON line (metric/value/... plus "roofline" for the dominant
-kernel and, at N = 1, "cpu_baseline": the numpy oracle on a bounded sample of
-the same workload on host cores).
+kernel, "parity_rel" of two sampled partitions against the CPU oracle after
+the timed region, and, at N = 1, "cpu_baseline": the numpy oracle on a
+bounded sample of the same workload on host cores, timed by wall clock).
 """
 
 from __future__ import annotations
@@ -41,65 +46,116 @@ FP64_MFMA_PEAK_TF = 78.6   # MI355X fp64 matrix (spec; = fp64 vector on CDNA4)
 
 CONFIGS = {
     2: dict(n=100_000_000, p=100, K=1024, family="logistic",
-            name="config2: synthetic logistic n=1e8 rows/GPU, p=100, K=1024 partitions/GPU"),
+            name="config2: synthetic logistic n=1e8, p=100, K=1024 partitions"),
     3: dict(n=15_000_000, p=181, K=128, family="logistic", data="dummy", intercept=True,
-            name="config3: airline-like logistic n=1.5e7 rows/GPU (1.2e8 on 8 GPUs), 9 numeric + "
-                 "172 dummy columns + intercept, K=128 partitions/GPU"),
+            name="config3: airline-like logistic n=1.5e7 (1.2e8 on 8 GPUs), 9 numeric + "
+                 "172 dummy columns + intercept, K=128 partitions"),
     5: dict(n=5_000_000, p=500, K=32, family="logistic",
-            name="config5: synthetic logistic n=5e6 rows/GPU, p=500, K=32 partitions/GPU (wide path)"),
+            name="config5: synthetic logistic n=5e6, p=500, K=32 partitions (wide path)"),
     4: dict(n=125_000_000, p=64, K=128, family="ols",
-            name="config4: synthetic OLS n=1.25e8 rows/GPU (1e9 on 8 GPUs), p=64, K=128 partitions/GPU"),
+            name="config4: synthetic OLS n=1.25e8 (1e9 on 8 GPUs), p=64, K=128 partitions"),
 }
 
 
-def _cpu_worker(args):
-    """One partition of the CPU baseline: regenerate its rows from the counter
-    stream, fit with the numpy oracle (1 BLAS thread)."""
-    n, p, seed, row0, family, data = args
+# ---------------------------------------------------------------------------
+# CPU baseline: the numpy oracle (port) on host cores, wall clock
+# ---------------------------------------------------------------------------
+
+
+def _cpu_worker(jobs, family, data, barrier, t_done, idx):
+    """Generate this worker's partitions (not timed), wait for every worker,
+    then fit them with the numpy oracle (1 BLAS thread) and record the
+    wall-clock finish time."""
     import numpy as np
     from threadpoolctl import threadpool_limits
 
     import oracle as O
 
     with threadpool_limits(1):
-        if data == "dummy":
-            import torch
+        parts = []
+        for (n, p, seed, row0) in jobs:
+            if data == "dummy":
+                import torch
 
-            from dlsa_amd.models import simulate_dummy_design
-            torch.set_num_threads(1)
-            Xt, yt = simulate_dummy_design(n, seed=seed + row0, device="cpu")
-            X, y = Xt.numpy(), yt.numpy()
-            X = np.hstack([np.ones((n, 1)), X])  # intercept column
-        else:
-            X, y = O.simulate_counter(n, p, seed=seed, row0=row0)
-        t0 = time.perf_counter()
-        if family == "ols":
-            O.ols_fit(X, y)
-            it = 1
-        else:
-            it = int(O.logistic_fit(X, y)["iters"])
-        return time.perf_counter() - t0, it
+                from dlsa_amd.models import simulate_dummy_design
+                torch.set_num_threads(1)
+                Xt, yt = simulate_dummy_design(n, seed=seed + row0, device="cpu")
+                X, y = Xt.numpy(), yt.numpy()
+                X = np.hstack([np.ones((n, 1)), X])  # intercept column
+            else:
+                X, y = O.simulate_counter(n, p, seed=seed, row0=row0)
+                if family == "ols":
+                    y = X[:, : max(1, int(0.4 * p))].sum(1) + 0.5 * (y - 0.5)
+            parts.append((X, y))
+        barrier.wait()
+        for X, y in parts:
+            if family == "ols":
+                O.ols_fit(X, y)
+            else:
+                O.logistic_fit(X, y)
+        t_done[idx] = time.time()
 
 
 def cpu_baseline(nk, p, n_parts, workers, family, seed=2019, data="counter"):
-    """Oracle (port) timed on host cores: n_parts partitions of nk rows, one
-    process per core, fit time only (data regeneration excluded)."""
+    """Oracle (port) timed on host cores: n_parts partitions of nk rows dealt
+    to `workers` processes (1 BLAS thread each).  Every worker generates its
+    data first (untimed); the clock runs from the barrier that releases all
+    workers to the last worker's finish: rows / wall time."""
     import multiprocessing as mp
 
     ctx = mp.get_context("spawn")
-    jobs = [(nk, p, seed, k * nk, family, data) for k in range(n_parts)]
-    t0 = time.perf_counter()
-    with ctx.Pool(workers) as pool:
-        res = pool.map(_cpu_worker, jobs, chunksize=1)
-    wall = time.perf_counter() - t0
-    fit_s = sum(r[0] for r in res)
-    rows_per_s = n_parts * nk / (fit_s / workers)  # all `workers` cores fitting concurrently
-    return {"value": rows_per_s, "unit": "rows/s", "cores": workers, "kind": "port",
-            "sample": f"{n_parts} partitions x {nk} rows x p={p}{' (dummy design + intercept)' if data == 'dummy' else ''}, numpy fp64 "
-                      f"{'OLS' if family == 'ols' else 'IRLS'} oracle, 1 BLAS thread per process, "
-                      f"{workers} processes; fit CPU time {fit_s:.1f} s, wall {wall:.1f} s incl. "
-                      f"data regeneration",
-            "iters_mean": sum(r[1] for r in res) / len(res)}
+    barrier = ctx.Barrier(workers + 1)
+    t_done = ctx.Array("d", workers)
+    jobs = [[] for _ in range(workers)]
+    for k in range(n_parts):
+        jobs[k % workers].append((nk, p, seed, k * nk))
+    procs = [ctx.Process(target=_cpu_worker, args=(jobs[w], family, data, barrier, t_done, w))
+             for w in range(workers)]
+    for pr in procs:
+        pr.start()
+    barrier.wait()
+    t0 = time.time()
+    for pr in procs:
+        pr.join()
+    wall = max(t_done[:]) - t0
+    return {"value": n_parts * nk / wall, "unit": "rows/s", "cores": workers, "kind": "port",
+            "sample": f"{n_parts} partitions x {nk} rows x p={p}"
+                      f"{' (dummy design + intercept)' if data == 'dummy' else ''}, numpy fp64 "
+                      f"{'OLS' if family == 'ols' else 'IRLS (tol 1e-12)'} oracle, 1 BLAS thread "
+                      f"per process, {workers} processes; wall clock {wall:.1f} s from the start "
+                      f"barrier to the last finish (data generation excluded)"}
+
+
+# ---------------------------------------------------------------------------
+# parity of sampled partitions (the oracle as the checker, after timing)
+# ---------------------------------------------------------------------------
+
+
+def sampled_parity(fit, X, y, offsets, family, codes=None, levels=None, fit_intercept=False,
+                   sample=None):
+    """max relative error (theta, Sig_inv) of the sampled partitions against
+    the CPU oracle; relative to the largest entry, as the GPU tests."""
+    import numpy as np
+
+    import oracle as O
+
+    K = len(offsets) - 1
+    sample = sample if sample is not None else sorted({0, K - 1})
+    worst = 0.0
+    for k in sample:
+        a, b = int(offsets[k]), int(offsets[k + 1])
+        Xk = X[a:b].cpu().numpy()
+        yk = y[a:b].cpu().numpy()
+        if codes is not None:
+            Xk = O.expand_codes(Xk, codes[a:b].cpu().numpy(), levels)
+        if family == "ols":
+            o = O.ols_fit(Xk, yk, fit_intercept=fit_intercept)
+        else:
+            o = O.logistic_fit(Xk, yk, fit_intercept=fit_intercept)
+        for got, ref in ((fit.theta[k], o["coef"]), (fit.sig_inv[k], o["Sig_inv"])):
+            g = got.cpu().numpy()
+            worst = max(worst, float(np.abs(g - ref).max() / np.abs(ref).max()))
+    return worst, sample
 
 
 def main():
@@ -108,13 +164,17 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
-    ap.add_argument("--n", type=int, default=0, help="rows per GPU (0: the config's)")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: the config's n and K per GPU; strong: n and K of the whole job, "
+                         "partitions sharded over the ranks")
+    ap.add_argument("--n", type=int, default=0, help="rows (per GPU, or total when strong)")
     ap.add_argument("--p", type=int, default=0)
-    ap.add_argument("--partitions", type=int, default=0, help="partitions per GPU")
+    ap.add_argument("--partitions", type=int, default=0)
     ap.add_argument("--hessian", default="mixed", choices=["mixed", "fp64", "mixed_f32"])
     ap.add_argument("--tol", type=float, default=1e-10)
     ap.add_argument("--cpu-parts", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--seed", type=int, default=2019)
     ap.add_argument("--layout", default="codes", choices=["codes", "dense"],
                     help="config 3: categorical-code layout (LDS-histogram pass) or the dense "
@@ -138,19 +198,34 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from dlsa_amd import _hip
+    from dlsa_amd.distributed import combine
     from dlsa_amd.dlsa import reduce_partitions_device, split_reduced, wlse
     from dlsa_amd.lsa import lars_lsa
     from dlsa_amd.models import (logistic_model_batched, logistic_model_batched_categorical,
                                  ols_model_batched, simulate_categorical, simulate_dummy_design,
                                  simulate_logistic_device)
 
-    n, p, K, family = cfg["n"], cfg["p"], cfg["K"], cfg["family"]
+    p, family = cfg["p"], cfg["family"]
     data = cfg.get("data", "counter")
     fit_intercept = bool(cfg.get("intercept", False))
     P = p + int(fit_intercept)
     wide = P > _hip.MAX_P_FUSED
-    offsets = (np.arange(K + 1, dtype=np.int64) * n) // K
+    if args.scaling == "strong":
+        n_job, K_job = cfg["n"], cfg["K"]
+        if K_job < world:
+            raise SystemExit("strong scaling needs at least one partition per rank")
+        goff = (np.arange(K_job + 1, dtype=np.int64) * n_job) // K_job
+        k0, k1 = rank * K_job // world, (rank + 1) * K_job // world
+        row0, n = int(goff[k0]), int(goff[k1] - goff[k0])
+        offsets = goff[k0:k1 + 1] - goff[k0]
+        K = k1 - k0
+    else:
+        n, K = cfg["n"], cfg["K"]
+        n_job, K_job = n * world, K * world
+        row0 = rank * n
+        offsets = (np.arange(K + 1, dtype=np.int64) * n) // K
     codes_layout = data == "dummy" and args.layout == "codes"
+    codes = levels = None
     if codes_layout:
         X, codes, y, levels = simulate_categorical(n, seed=args.seed + rank, device=dev)
         assert X.shape[1] + int((levels - 1).sum()) == p
@@ -158,13 +233,12 @@ def main():
         X, y = simulate_dummy_design(n, seed=args.seed + rank, device=dev)
         assert X.shape[1] == p
     else:
-        X, y = simulate_logistic_device(n, p, seed=args.seed, row0=rank * n, device=dev)
+        X, y = simulate_logistic_device(n, p, seed=args.seed, row0=row0, device=dev)
     if family == "ols":  # linear response on the same design
         y = X[:, : max(1, int(0.4 * p))].sum(1) + 0.5 * (y - 0.5)
     ws = torch.empty((1,), dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
 
-    n_global = n * world
     stats_acc = []
 
     def step(record):
@@ -181,15 +255,15 @@ def main():
                                          record_timing=record, workspace=ws, device=dev)
             if ws.numel() < fit.stats["workspace_bytes"]:
                 ws = torch.empty((fit.stats["workspace_bytes"],), dtype=torch.uint8, device=dev)
-        buf = reduce_partitions_device(fit)
-        if world > 1:
-            dist.all_reduce(buf, op=dist.ReduceOp.SUM)  # RCCL over xGMI
-        S, v, st, Ksum = split_reduced(buf.cpu().numpy(), fit.P)
+        buf = reduce_partitions_device(fit, n_rows=True)
+        combine(buf)  # the one collective: RCCL all-reduce over xGMI (no-op at N = 1)
+        b = buf.cpu().numpy()
+        S, v, st, Ksum = split_reduced(b[:-1], fit.P)
         est = wlse(S, v)
-        lars = lars_lsa(S, est, fit_intercept, n_global, type="lasso")
+        lars = lars_lsa(S, est, fit_intercept, int(round(b[-1])), type="lasso")
         ib = int(np.argmin(lars["BIC"]))
         support = np.nonzero(lars["beta"][ib])[0]
-        return fit, est, support
+        return fit, est, support, int(round(Ksum)), int(round(b[-1]))
 
     for _ in range(args.warmup):
         step(False)
@@ -198,7 +272,7 @@ def main():
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        fit, est, support = step(True)
+        fit, est, support, K_red, n_red = step(True)
         stats_acc.append(fit.stats)
     torch.cuda.synchronize()
     if world > 1:
@@ -208,8 +282,9 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
+    assert K_red == K_job and n_red == n_job, (K_red, n_red, K_job, n_job)
     ms_per_step = elapsed / args.steps * 1e3
-    value = n_global * args.steps / elapsed
+    value = n_job * args.steps / elapsed
 
     # ---- per-kernel throughput and the roofline of the dominant kernel -----
     # (HIP events recorded on the fit's stream around every launch)
@@ -219,6 +294,14 @@ def main():
         row_bytes = 8 * X.shape[1] + codes.shape[1] + 8
     alg_flops_row = P * (P + 1) + 4 * P + 20     # symmetric X^T W X + X.b, X^T r
     kern = {}
+
+    def hbm_roof(kname, ms, launches, rows):
+        achieved = rows * row_bytes / (ms * 1e-3) / 1e9
+        return {"kernel": kname, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                "algorithmic_bytes_per_launch": rows * row_bytes / launches,
+                "rows_per_launch": rows / launches, "avg_launch_ms": ms / launches}
+
     if codes_layout:
         ms64, n64, rows64 = tot("ms_pass_fp64"), tot("passes_fp64"), tot("rows_fp64")
         kern["cat_pass_kernel"] = {
@@ -227,14 +310,10 @@ def main():
             "GBps": rows64 * row_bytes / (ms64 * 1e-3) / 1e9,
             "Grows_per_s": rows64 / (ms64 * 1e-3) / 1e9}
         kern["newton_solve"] = {"ms_per_step": tot("ms_solve") / args.steps}
-        achieved = rows64 * row_bytes / (ms64 * 1e-3) / 1e9
-        roof = {"kernel": "cat_pass_kernel (categorical codes, one-hot blocks as fp64 LDS "
-                          "histograms)", "bound": "hbm", "achieved": achieved,
-                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None, "algorithmic_bytes_per_launch": rows64 * row_bytes / n64,
-                "avg_launch_ms": ms64 / n64,
-                "note": "bytes/row = 8 q + F + 8 (codes layout); the kernel issues ~47 fp64 "
-                        "LDS atomics per row, which bound it before HBM"}
+        roof = hbm_roof("cat_pass_kernel (categorical codes, one-hot blocks as fp64 LDS "
+                        "histograms)", ms64, n64, rows64)
+        roof["note"] = "bytes/row = 8 q + F + 8 (codes layout)"
+        pmc_key = "cat_pass_kernel"
     elif wide:
         NB = (P + 127) // 128
         gram_flops_row = NB * (NB + 1) // 2 * 128 * 128 * 2  # issued MFMA work per row
@@ -246,6 +325,7 @@ def main():
         if n32:
             kern["wide_gram_bf16_kernel"] = {
                 "launches_per_step": n32 / args.steps, "avg_launch_ms": ms32 / n32,
+                "GBps": rows32 * row_bytes / (ms32 * 1e-3) / 1e9,
                 "alg_TFps": rows32 * p * (p + 1) / (ms32 * 1e-3) / 1e12,
                 "mfma_TFps": rows32 * gram_flops_row / (ms32 * 1e-3) / 1e12}
         if n64:
@@ -261,21 +341,20 @@ def main():
                     "achieved": achieved, "peak": FP64_MFMA_PEAK_TF, "unit": "TFLOP/s",
                     "frac": achieved / FP64_MFMA_PEAK_TF, "traffic": None,
                     "algorithmic_flops_per_launch": rows64 * p * (p + 1) / n64,
-                    "avg_launch_ms": ms64 / n64,
+                    "rows_per_launch": rows64 / n64, "avg_launch_ms": ms64 / n64,
                     "mfma_issued_TFps": rows64 * gram_flops_row / (ms64 * 1e-3) / 1e12}
+            pmc_key = "wide_gram_kernel<fp64>"
         else:
-            achieved = rows32 * row_bytes / (ms32 * 1e-3) / 1e9
-            roof = {"kernel": "wide_gram_bf16_kernel (approximate X^T W X)", "bound": "hbm",
-                    "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                    "algorithmic_bytes_per_launch": rows32 * row_bytes / n32,
-                    "avg_launch_ms": ms32 / n32}
+            roof = hbm_roof("wide_gram_bf16_kernel (approximate X^T W X)", ms32, n32, rows32)
+            pmc_key = "wide_gram_bf16_kernel"
     else:
         NT = (P + 15) // 16
         mfma_flops_per_row = NT * (NT + 1) // 2 * 16 * 16 * 2  # lower-triangle 16x16 tiles
         ms32, ms64 = tot("ms_pass_fp32"), tot("ms_pass_fp64")
         n32, n64 = tot("passes_fp32"), tot("passes_fp64")
         rows32, rows64 = tot("rows_fp32"), tot("rows_fp64")
+        exact = (f"irls_wave_kernel<NT={NT},fp64> (per-wave exact pass)" if NT <= 8
+                 else f"irls_coop_kernel<NT={NT},fp64 Hessian>")
         if n32:
             kern["irls_coop<bf16 Hessian>"] = {
                 "launches_per_step": n32 / args.steps, "ms_per_step": ms32 / args.steps,
@@ -283,36 +362,45 @@ def main():
                 "GBps": rows32 * row_bytes / (ms32 * 1e-3) / 1e9,
                 "mfma_TFps": rows32 * mfma_flops_per_row / (ms32 * 1e-3) / 1e12}
         if n64:
-            kern["irls_coop<fp64 Hessian>"] = {
+            kern[exact] = {
                 "launches_per_step": n64 / args.steps, "ms_per_step": ms64 / args.steps,
                 "avg_launch_ms": ms64 / n64, "rows_per_launch": rows64 / n64,
                 "GBps": rows64 * row_bytes / (ms64 * 1e-3) / 1e9,
-                "mfma_TFps": rows64 * mfma_flops_per_row / (ms64 * 1e-3) / 1e12}
+                "alg_TFps": rows64 * alg_flops_row / (ms64 * 1e-3) / 1e12,
+                "mfma_TFps": rows64 * mfma_flops_per_row / (ms64 * 1e-3) / 1e12,
+                "mfma_frac": rows64 * mfma_flops_per_row / (ms64 * 1e-3) / 1e12
+                / FP64_MFMA_PEAK_TF}
         kern["newton_solve"] = {"ms_per_step": tot("ms_solve") / args.steps}
         if ms32 >= ms64:
-            achieved = rows32 * row_bytes / (ms32 * 1e-3) / 1e9
-            roof = {"kernel": f"irls_coop_kernel<NT={NT},bf16 Hessian> (approximate-Hessian passes)",
-                    "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                    "algorithmic_bytes_per_launch": rows32 * row_bytes / n32,
-                    "avg_launch_ms": ms32 / n32}
+            roof = hbm_roof(f"irls_coop_kernel<NT={NT},bf16 Hessian> (approximate-Hessian "
+                            "passes)", ms32, n32, rows32)
+            pmc_key = "irls_coop<bf16>"
+        elif family == "ols":
+            # config 4 is HBM-bound (65 GB vs 0.54 TF per GPU)
+            roof = hbm_roof(exact + " (OLS: X^T X, X^T y in one pass)", ms64, n64, rows64)
+            roof["mfma_issued_frac"] = kern[exact]["mfma_frac"]
+            pmc_key = "irls_wave<ols>"
         else:
             achieved = rows64 * mfma_flops_per_row / (ms64 * 1e-3) / 1e12
-            kname = (f"irls_wave_kernel<NT={NT},fp64> (per-wave exact pass)" if NT <= 8
-                     else f"irls_coop_kernel<NT={NT},fp64 Hessian>")
-            roof = {"kernel": kname, "bound": "mfma",
-                    "achieved": achieved, "peak": FP64_MFMA_PEAK_TF, "unit": "TFLOP/s",
+            roof = {"kernel": exact, "bound": "mfma", "achieved": achieved,
+                    "peak": FP64_MFMA_PEAK_TF, "unit": "TFLOP/s",
                     "frac": achieved / FP64_MFMA_PEAK_TF, "traffic": None,
                     "mfma_flops_per_launch": rows64 * mfma_flops_per_row / n64,
-                    "avg_launch_ms": ms64 / n64,
-                    "GBps": rows64 * row_bytes / (ms64 * 1e-3) / 1e9}
+                    "rows_per_launch": rows64 / n64, "avg_launch_ms": ms64 / n64}
+            pmc_key = "irls_wave<fp64>"
+    # HBM traffic from the PMC passes (tools/pmc.sh + tools/pmc_summary.py):
+    # bytes per row of a full-pass launch of this kernel at this p, scaled to
+    # this run's rows per launch, so traffic and the algorithmic bytes
+    # describe the same launch
     pmc_file = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_file):
         try:
-            pmc = json.load(open(pmc_file)).get(f"config{args.config}", {})
-            if pmc.get("p") == p and pmc.get("n") == n and pmc.get("kernel") == roof["kernel"]:
-                roof["traffic"] = pmc["hbm_bytes_per_launch"]
-                roof["traffic_source"] = pmc.get("source")
+            rec = json.load(open(pmc_file)).get(f"config{args.config}", {})
+            if rec.get("p") == p and rec.get("kernel_key") == pmc_key:
+                roof["traffic"] = rec["hbm_bytes_per_row"] * roof["rows_per_launch"]
+                roof["traffic_bytes_per_row"] = rec["hbm_bytes_per_row"]
+                roof["algorithmic_bytes_per_row"] = row_bytes
+                roof["traffic_source"] = rec.get("source")
         except Exception:
             pass
 
@@ -320,7 +408,7 @@ def main():
     out = {
         "metric": METRIC, "value": value, "unit": "rows/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f64",
         "data": ("synthetic airline-like: 9 U(-1/2,1/2) numeric + dummies of 5 skewed factors "
                  "(12/7/20/69/69 levels, baseline dropped), y~Bernoulli(sigmoid(-0.3+X beta*)); "
                  "torch generator in HBM (not timed); layout: " +
@@ -328,13 +416,17 @@ def main():
                   "dense dummy design")) if data == "dummy" else
                 "synthetic: X~U(-1/2,1/2), beta*=1 on first floor(0.4p) cols, y~Bernoulli"
                 "(sigmoid(X beta*)); counter-based generator in HBM (not timed)",
-        "config": {"workload": cfg["name"] + " + DLSA combine + LARS/DBIC",
-                   "n_rows_per_gpu": n, "p": p, "P": P, "fit_intercept": fit_intercept,
+        "config": {"workload": cfg["name"] + (" per GPU" if args.scaling == "weak" else
+                                              " in total") + " + DLSA combine + LARS/DBIC",
+                   "n_rows_job": n_job, "n_rows_per_gpu": n, "p": p, "P": P,
+                   "fit_intercept": fit_intercept, "partitions_job": K_job,
                    "partitions_per_gpu": K,
                    **({"layout": args.layout} if data == "dummy" else {}),
-                   "family": family, "hessian": args.hessian if family == "logistic" and not codes_layout else "fp64",
+                   "family": family,
+                   "hessian": args.hessian if family == "logistic" and not codes_layout else "fp64",
                    "tol": args.tol,
-                   "parallelism": f"dp{world} (partitions sharded; 1 RCCL all-reduce of P^2+2P+1 fp64)"},
+                   "parallelism": f"dp{world} (partitions sharded; 1 RCCL all-reduce of "
+                                  "P^2+2P+2 fp64)"},
         "roofline": roof,
         "kernels": kern,
         "newton": {"iterations": last["iterations"], "passes_fp32": last["passes_fp32"],
@@ -343,6 +435,14 @@ def main():
         "dbic_support_size": int(len(support)),
         "algorithmic": {"bytes_per_pass": n * row_bytes, "flops_per_pass": n * alg_flops_row},
     }
+    if rank == 0 and not args.no_parity:
+        # checker, after the timed region: the last step's fit of this rank
+        sample = [0] if wide else None
+        rel, smp = sampled_parity(fit, X, y, offsets, family, codes=codes, levels=levels,
+                                  fit_intercept=fit_intercept, sample=sample)
+        out["parity_rel"] = rel
+        out["parity_sample"] = (f"partitions {smp} of rank 0 vs the numpy oracle (tol 1e-12): "
+                                "max |diff| / max |ref| over theta and Sig_inv")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         workers = min(16, os.cpu_count() or 1)
         if args.config == 5:

@@ -24,7 +24,13 @@ def combine(buf, group=None):
     import torch.distributed as dist
 
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-        dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
+        if buf.is_cuda and dist.get_backend(group) == "gloo":
+            # gloo (CPU test / fallback transport): reduce a host copy
+            tmp = buf.cpu()
+            dist.all_reduce(tmp, op=dist.ReduceOp.SUM, group=group)
+            buf.copy_(tmp)
+        else:
+            dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
     return buf
 
 

@@ -104,7 +104,10 @@ def read_csv_partitioned(path, Y_name, usecols_x, K=None, sample_size_per_partit
     dict with ``X`` [n, p] fp64 (columns ``usecols_x`` in order), ``y``,
     ``offsets``, ``columns``; with it, the categorical-code layout of
     ``encode_categorical`` (``Xn``, ``codes``, ``levels``, ``cols``, ...) for
-    ``logistic_model_batched_categorical``."""
+    ``logistic_model_batched_categorical``; ``zero_partitions`` lists the
+    partitions holding a factor value that is neither selected nor a baseline
+    (their rows are coded as the baseline; pass the list on to the fit, which
+    returns the reference's zero frame for them, models.py:84-91)."""
     dev = _require_gpu(device)
     df = read_table(path, Y_name, usecols_x)
     n = len(df)
@@ -121,8 +124,9 @@ def read_csv_partitioned(path, Y_name, usecols_x, K=None, sample_size_per_partit
         Xn = torch.from_numpy(enc["Xn"]).pin_memory().to(dev, non_blocking=True)
         codes = torch.from_numpy(enc["codes"]).pin_memory().to(dev, non_blocking=True)
         (Xp, cp, yp), offsets = repartition(pid, K, Xn, codes, y, device=dev)
+        zero = np.unique(np.nonzero(enc["unknown_rows"])[0] % K).astype(np.int64)
         return {"Xn": Xp, "codes": cp, "y": yp, "offsets": offsets, "levels": enc["levels"],
-                "numeric": enc["numeric"], "cols": enc["cols"], "K": K}
+                "numeric": enc["numeric"], "cols": enc["cols"], "K": K, "zero_partitions": zero}
     X = torch.from_numpy(np.ascontiguousarray(df[list(usecols_x)].to_numpy(dtype=np.float64)))
     X = X.pin_memory().to(dev, non_blocking=True)
     (Xp, yp), offsets = repartition(pid, K, X, y, device=dev)

@@ -187,7 +187,8 @@ def encode_categorical(sample_df, Y_name, dummy_info, dummy_factors_baseline=())
     ``levels`` [F] int32 (= dummy columns + 1), ``numeric`` / ``cols`` (the
     reference's column names, intercept excluded), ``unknown`` (a value outside
     the selected and baseline names: the reference's column-set check fails,
-    models.py:84) and ``counts`` (rows per dummy column)."""
+    models.py:84), ``unknown_rows`` ([n] bool: the rows holding such a value)
+    and ``counts`` (rows per dummy column)."""
     factors = list(dummy_info["factor_selected"].keys())
     dropped = {k: v for k, v in dummy_info["factor_dropped"].items() if len(v) > 0}
     df = sample_df.replace(dropped, "000_OTHERS") if dropped else sample_df
@@ -198,6 +199,7 @@ def encode_categorical(sample_df, Y_name, dummy_info, dummy_factors_baseline=())
     levels = np.zeros(len(factors), dtype=np.int32)
     cols = list(numeric)
     unknown = False
+    unknown_rows = np.zeros(n, dtype=bool)
     counts = []
     for fi, f in enumerate(factors):
         names = [c for c in sorted(dummy_info["factor_selected_names"][f]) if c not in base]
@@ -216,6 +218,7 @@ def encode_categorical(sample_df, Y_name, dummy_info, dummy_factors_baseline=())
         c = mapped[inv] if n else np.zeros(0, dtype=np.int64)
         if (c < 0).any():
             unknown = True
+            unknown_rows |= c < 0
             c = np.where(c < 0, 0, c)
         codes[:, fi] = c
         levels[fi] = len(names) + 1
@@ -224,7 +227,7 @@ def encode_categorical(sample_df, Y_name, dummy_info, dummy_factors_baseline=())
     Xn = np.ascontiguousarray(df[numeric].to_numpy(dtype=np.float64)) if numeric else \
         np.zeros((n, 0), dtype=np.float64)
     return {"Xn": Xn, "codes": codes, "levels": levels, "numeric": numeric, "cols": cols,
-            "unknown": unknown,
+            "unknown": unknown, "unknown_rows": unknown_rows,
             "counts": np.concatenate(counts) if counts else np.zeros(0, dtype=np.int64)}
 
 
@@ -351,7 +354,8 @@ def logistic_model_batched(X, y, offsets, fit_intercept=False, center=None, scal
 
 def logistic_model_batched_categorical(Xn, codes, y, offsets, levels, fit_intercept=False,
                                        center=None, scale=None, max_iter=100, tol=1e-10,
-                                       record_timing=False, rows_per_chunk=0, device=None):
+                                       record_timing=False, rows_per_chunk=0, zero_partitions=None,
+                                       device=None):
     """Batched local logistic fit on the categorical-code layout (the dummy
     branch of dlsa/models.py:56-91, BASELINE config 3) without materialising
     the dummy matrix: the one-hot blocks of X^T W X are LDS histograms in the
@@ -362,7 +366,11 @@ def logistic_model_batched_categorical(Xn, codes, y, offsets, levels, fit_interc
     + 1); ``center``/``scale`` [q] standardise the numeric columns only
     (models.py:99-101).  Parameters: [intercept] [numeric] [factor 0 dummies]
     ...  A partition with a dummy column that has no rows gets status
-    "missing_level" and all-zero outputs (the reference's zero frame)."""
+    "missing_level" and all-zero outputs (the reference's zero frame), and so
+    does every partition listed in ``zero_partitions`` (the partitions holding
+    a factor value outside dummy_info, ``read_csv_partitioned``'s
+    ``zero_partitions``: the reference's column-set check fails there too,
+    models.py:84-91)."""
     dev = _require_gpu(device)
     Xd = _dev_f64(Xn, dev)
     if Xd.dim() != 2:
@@ -406,8 +414,13 @@ def logistic_model_batched_categorical(Xn, codes, y, offsets, levels, fit_interc
         int(max_iter), float(tol), _ptr(theta), _ptr(sig), _ptr(sigt), _ptr(ll), _ptr(iters),
         _ptr(status), ctypes.byref(opt), _stream(dev))
     _hip.check(rc, "dlsa_logistic_fit_categorical")
-    return BatchedFit(theta, sig, sigt, ll, iters, status, offs, bool(fit_intercept),
-                      _hip.last_fit_stats())
+    stats = _hip.last_fit_stats()
+    if zero_partitions is not None and len(zero_partitions):
+        idx = torch.as_tensor(np.asarray(zero_partitions, dtype=np.int64), device=dev)
+        for t in (theta, sig, sigt, ll):
+            t[idx] = 0
+        status[idx] = 5
+    return BatchedFit(theta, sig, sigt, ll, iters, status, offs, bool(fit_intercept), stats)
 
 
 def ols_model_batched(X, y, offsets, fit_intercept=False, center=None, scale=None,

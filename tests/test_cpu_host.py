@@ -339,3 +339,20 @@ def test_encode_categorical_missing_value_is_all_zero_block():
     assert e["cols"] == list(ref.columns)
     assert np.array_equal(O.expand_codes(e["Xn"], e["codes"], e["levels"]),
                           ref.to_numpy(dtype=np.float64))
+
+
+def test_encode_categorical_unknown_rows():
+    """A value outside the selected names and the baselines is flagged per
+    row (the reference's column-set check, models.py:84): its row is coded 0
+    and reported in ``unknown_rows``."""
+    import pandas as pd
+
+    from dlsa_amd.models import encode_categorical
+
+    df = pd.DataFrame({"partition_id": [0.0] * 5, "y": [0, 1, 0, 1, 1.0],
+                       "F": ["a", "b", "zz", "c", "a"], "x": [1, 2, 3, 4, 5.0]})
+    di = {"factor_selected": {"F": ["a", "b", "c"]}, "factor_dropped": {"F": []},
+          "factor_selected_names": {"F": ["F_a", "F_b", "F_c"]}}
+    e = encode_categorical(df, "y", di, ["F_a"])
+    assert e["unknown"] and e["unknown_rows"].tolist() == [False, False, True, False, False]
+    assert e["codes"][:, 0].tolist() == [0, 1, 0, 2, 0]

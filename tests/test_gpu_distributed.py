@@ -1,0 +1,71 @@
+"""The product's sharded path end to end with world_size 2 on the GPU box:
+two processes (ranks) on the one visible MI355X, each fitting its own
+partitions in HBM (dlsa_fit_sharded: batched fit -> HBM pre-reduction ->
+ONE all-reduce carrying the sums, K and N -> WLSE / ONESHOT / LARS / DBIC),
+gloo as the transport (RCCL needs one GPU per rank; the driver's 8-GPU bench
+runs the same code over nccl = RCCL).  Every rank must get the reference's
+config-1 golden WLSE, ONESHOT and DBIC support."""
+
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _worker(rank, world, port, golden_dir, shards, q):
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dlsa_amd.distributed import dlsa_fit_sharded
+
+        g = np.load(os.path.join(golden_dir, "config1_n1e5_p10_K4.npz"))
+        np.random.seed(int(g["seed"]))
+        pid, lab, feat = O.simulate_logistic_arrays(100000, 10, "systematic", 4)
+        order, off = O.systematic_partition(pid)
+        X, y = feat[order], lab[order]
+        mine = shards[rank]
+        Xl = np.concatenate([X[off[k]:off[k + 1]] for k in mine])
+        yl = np.concatenate([y[off[k]:off[k + 1]] for k in mine])
+        offl = np.concatenate([[0], np.cumsum([off[k + 1] - off[k] for k in mine])])
+        res = dlsa_fit_sharded(torch.from_numpy(Xl).cuda(), torch.from_numpy(yl).cuda(), offl)
+        q.put((rank, res["wlse"], res["oneshot"], res["dbic_support"].tolist(),
+               res["fit"].theta.cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("shards", [([0, 2], [1, 3]), ([3], [0, 1, 2])])
+def test_sharded_fit_two_ranks_one_gpu(golden_dir, shards):
+    import multiprocessing as mp
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, golden_dir, shards, q)) for r in range(2)]
+    for p_ in ps:
+        p_.start()
+    res = [q.get(timeout=180) for _ in range(2)]
+    for p_ in ps:
+        p_.join(timeout=60)
+        assert p_.exitcode == 0
+    g = np.load(os.path.join(golden_dir, "config1_n1e5_p10_K4.npz"))
+    gb = g["lars_lasso_beta"][int(np.argmin(g["lars_lasso_BIC"]))]
+    for rank, wlse, oneshot, support, theta in res:
+        assert np.abs(wlse - g["wlse_noint"]).max() / np.abs(g["wlse_noint"]).max() < 1e-8
+        assert np.abs(oneshot - g["oneshot_noint"]).max() / np.abs(g["oneshot_noint"]).max() < 1e-8
+        assert support == np.nonzero(gb)[0].tolist()
+        ref = g["outs_noint"][shards[rank]][:, :, 1]
+        assert np.abs(theta - ref).max() / np.abs(ref).max() < 1e-8

@@ -137,3 +137,46 @@ def test_read_csv_partitioned_dummies(torch_cuda, tmp_path, golden_dir):
         assert np.abs(fit.theta[k].cpu().numpy() - r["coef"]).max() / np.abs(r["coef"]).max() < 1e-8
         assert np.abs(fit.sig_inv[k].cpu().numpy() - r["Sig_inv"]).max() / \
             np.abs(r["Sig_inv"]).max() < 1e-8
+
+
+def test_read_csv_partitioned_unknown_level_zero_frame(torch_cuda, tmp_path, golden_dir):
+    """A factor value that is neither selected nor a baseline (an airport
+    dummy_info has never seen): the reference's column-set check fails for
+    that chunk (models.py:84-91) and it returns the zero frame.  The ingest
+    reports the partition in ``zero_partitions`` and the fit returns the zero
+    frame with status missing_level there; the other partitions are fitted
+    as usual."""
+    from test_oracle_golden import _dummy_fixture
+
+    from dlsa_amd.ingest import read_csv_partitioned
+    from dlsa_amd.models import logistic_model_batched_categorical
+
+    g, df, dinfo, base, info = _dummy_fixture(golden_dir)
+    df = df[df["partition_id"] < 4].drop(columns=["partition_id"]).reset_index(drop=True)
+    df["Origin"] = df["Origin"].astype(str)
+    bad_row = 301
+    df.loc[bad_row, "Origin"] = "ZZZ_unseen"
+    df.to_csv(tmp_path / "u.csv", index=False)
+    cols = ["Month", "UniqueCarrier", "Origin", "Distance", "DepTime"]
+    lay = read_csv_partitioned(str(tmp_path / "u.csv"), "label", cols, K=3, dummy_info=dinfo,
+                               dummy_factors_baseline=base)
+    assert lay["zero_partitions"].tolist() == [bad_row % 3]
+    fit = logistic_model_batched_categorical(lay["Xn"], lay["codes"], lay["y"], lay["offsets"],
+                                             lay["levels"], fit_intercept=True,
+                                             zero_partitions=lay["zero_partitions"])
+    st = fit.status.cpu().numpy()
+    k0 = bad_row % 3
+    assert st[k0] == 5 and (np.delete(st, k0) == 0).all()
+    assert not fit.theta[k0].abs().max().item() and not fit.sig_inv[k0].abs().max().item()
+    order, off = O.systematic_partition(np.arange(len(df)) % 3)
+    d = df.iloc[order].reset_index(drop=True)
+    for k in range(3):
+        if k == k0:
+            continue
+        part = d.iloc[off[k]:off[k + 1]]
+        X, names, missing = O.dummy_design({c: part[c].to_numpy() for c in ("Distance", "DepTime")},
+                                           {c: part[c].to_numpy() for c in
+                                            ("Month", "UniqueCarrier", "Origin")}, dinfo, base)
+        assert not missing
+        r = O.logistic_fit(X, part["label"].to_numpy(float), fit_intercept=True)
+        assert np.abs(fit.theta[k].cpu().numpy() - r["coef"]).max() / np.abs(r["coef"]).max() < 1e-8

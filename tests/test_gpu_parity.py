@@ -580,3 +580,133 @@ def test_categorical_edge_layouts(torch_cuda, M, q, levels, fi):
     assert (fit.status.cpu().numpy() == 0).all(), fit.status
     assert _rel(fit.theta.cpu(), th) < REL
     assert _rel(fit.sig_inv.cpu(), S) < REL
+
+
+# ---------------------------------------------------------------------------
+# boundary, modes and failure handling
+# ---------------------------------------------------------------------------
+
+
+def test_plain_c_abi_entry_as_integration_binds_it(golden_dir, torch_cuda):
+    """dlsa_logistic_fit_batched exactly as INTEGRATION.md section 2 binds it
+    (a fresh ctypes.CDLL, its argtypes, K = 1 per call, the caller's stream)
+    reproduces the reference's config-1 partitions (models.py:42)."""
+    import ctypes
+
+    torch = torch_cuda
+    from dlsa_amd import _hip
+
+    lib = ctypes.CDLL(_hip.LIB_PATH)
+    v = ctypes.c_void_p
+    lib.dlsa_logistic_fit_batched.argtypes = [
+        v, v, v, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, v, v,
+        ctypes.c_int32, ctypes.c_double, v, v, v, v, v, v, v]
+    lib.dlsa_last_error.restype = ctypes.c_char_p
+    g, X, y, off = _config1(golden_dir)
+    for fi, tag in ((False, "noint"), (True, "int")):
+        for k in range(4):
+            xk = X[off[k]:off[k + 1]]
+            n, p = xk.shape
+            P = p + int(fi)
+            Xd = torch.from_numpy(np.ascontiguousarray(xk)).cuda()
+            Yd = torch.from_numpy(np.ascontiguousarray(y[off[k]:off[k + 1]])).cuda()
+            th = torch.empty(1, P, dtype=torch.float64, device="cuda")
+            S = torch.empty(1, P, P, dtype=torch.float64, device="cuda")
+            St = torch.empty(1, P, dtype=torch.float64, device="cuda")
+            ll = torch.empty(1, dtype=torch.float64, device="cuda")
+            it = torch.empty(1, dtype=torch.int32, device="cuda")
+            st = torch.empty(1, dtype=torch.int32, device="cuda")
+            offs = np.array([0, n], dtype=np.int64)
+            rc = lib.dlsa_logistic_fit_batched(
+                Xd.data_ptr(), Yd.data_ptr(), offs.ctypes.data, 1, p, int(fi), None, None, 100,
+                1e-10, th.data_ptr(), S.data_ptr(), St.data_ptr(), ll.data_ptr(), it.data_ptr(),
+                st.data_ptr(), torch.cuda.current_stream().cuda_stream)
+            assert rc == 0, lib.dlsa_last_error()
+            torch.cuda.synchronize()
+            ref = g["outs_" + tag][k]
+            assert int(st.item()) == 0
+            assert _rel(th[0].cpu(), ref[:, 1]) < REL
+            assert _rel(S[0].cpu(), ref[:, 3:]) < REL
+            assert _rel(St[0].cpu(), ref[:, 2]) < REL
+
+
+@pytest.mark.parametrize("p,fi", [(10, True), (100, False), (150, True), (300, False)])
+def test_hessian_mixed_f32_vs_oracle(torch_cuda, M, p, fi):
+    """hessian="mixed_f32" (fp32-MFMA approximate Hessian, fp64 gradient and
+    final pass) reaches the same MLE and Sig_inv as the oracle -- fused
+    (4- and 8-wave) and wide geometries."""
+    sizes = [4000 + 13 * p, 3000 + 11 * p]
+    n = sum(sizes)
+    X, y = O.simulate_counter(n, p, seed=p + 100 * fi)
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    fit = M.logistic_model_batched(X, y, off, fit_intercept=fi, hessian="mixed_f32",
+                                   rows_per_chunk=1500)
+    th, S, St, ll, it = O.logistic_fit_partitions(X, y, off, fit_intercept=fi)
+    assert (fit.status.cpu().numpy() == 0).all()
+    assert fit.stats["passes_fp32"] > 0 and fit.stats["passes_fp64"] > 0
+    assert _rel(fit.theta.cpu(), th) < REL
+    assert _rel(fit.sig_inv.cpu(), S) < REL
+    assert _rel(fit.sig_inv_theta.cpu(), St) < REL
+
+
+@pytest.mark.parametrize("w", ["1", "2"])
+@pytest.mark.parametrize("p,fi,std", [(17, False, False), (64, True, True), (100, False, False),
+                                      (111, True, False)])
+def test_exact_pass_wave_split_vs_oracle(torch_cuda, M, monkeypatch, w, p, fi, std):
+    """The per-wave exact pass in both geometries (DLSA_WAVE_W: all tiles in
+    one wave, or the tile rows split over two waves with the rows of a block
+    split in the row phase): fp64 fits and OLS against the oracle, with
+    standardisation, intercept and ragged partitions (block tails)."""
+    monkeypatch.setenv("DLSA_WAVE_W", w)
+    sizes = [3001, 1777, 4096 + 9]
+    n = sum(sizes)
+    X, y = O.simulate_counter(n, p, seed=3 * p + fi)
+    center = scale = None
+    if std:
+        X = X * 3.0 - 0.7
+        center, scale = X.mean(0), X.std(0)
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    fit = M.logistic_model_batched(X, y, off, fit_intercept=fi, center=center, scale=scale,
+                                   hessian="fp64", rows_per_chunk=1000)
+    th, S, St, ll, it = O.logistic_fit_partitions(X, y, off, fit_intercept=fi, center=center,
+                                                  scale=scale)
+    assert (fit.status.cpu().numpy() == 0).all()
+    assert _rel(fit.theta.cpu(), th) < REL
+    assert _rel(fit.sig_inv.cpu(), S) < REL
+    assert _rel(fit.loglik.cpu(), ll) < 1e-10
+    yl = X[:, :3].sum(1) + 0.1 * y
+    ols = M.ols_model_batched(X, yl, off, fit_intercept=fi, rows_per_chunk=1000)
+    for k in range(3):
+        o = O.ols_fit(X[off[k]:off[k + 1]], yl[off[k]:off[k + 1]], fit_intercept=fi)
+        assert _rel(ols.theta[k].cpu(), o["coef"]) < REL
+        assert _rel(ols.sig_inv[k].cpu(), o["Sig_inv"]) < 1e-12
+
+
+def test_nonfinite_partition_is_excluded_from_the_combine(torch_cuda, M):
+    """A partition with a NaN in X ends "nonfinite" with a finite theta (the
+    last finite iterate) and is summed as the reference's zero frame, with a
+    warning: WLSE / ONESHOT / DBIC of the others stay finite and equal to the
+    oracle's combine with that frame zeroed."""
+    from dlsa_amd.dlsa import dlsa_mapred
+
+    p = 6
+    sizes = [3000, 2500, 2800]
+    n = sum(sizes)
+    X, y = O.simulate_counter(n, p, seed=41)
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    Xb = X.copy()
+    Xb[off[1] + 17, 2] = np.nan
+    fit = M.logistic_model_batched(Xb, y, off)
+    st = fit.status.cpu().numpy()
+    assert st.tolist() == [0, 4, 0]
+    assert np.isfinite(fit.theta.cpu().numpy()).all()
+    with pytest.warns(UserWarning, match=r"partitions \[1\] ended \['nonfinite'\]"):
+        comb = dlsa_mapred(fit)
+    th, S, St, _, _ = O.logistic_fit_partitions(X, y, off)
+    th[1] = 0.0
+    S[1] = 0.0
+    St[1] = 0.0
+    wlse, oneshot, Ssum = O.dlsa_mapred(th, S, St)
+    assert _rel(comb["beta_byOLS"], wlse) < REL
+    assert _rel(comb["beta_byONESHOT"], oneshot) < REL
+    assert _rel(comb.iloc[:, 2:].to_numpy(), Ssum) < REL

@@ -1,60 +1,64 @@
 """Summarise a tools/pmc.sh run into profiles/.
 
-Reads gpurun_out/<tag>/p{1..4}/run_counter_collection.csv, writes
-profiles/<out>_pmc.csv (per-dispatch counters of the IRLS pass kernels) and
+Reads gpurun_out/<tag>/p{1..4}/**/*counter_collection.csv, writes
+profiles/<prefix>_pmc.csv (per-dispatch counters of the pass kernels) and
 updates profiles/pmc_traffic.json, the file bench.py reads for
-roofline.traffic.  HBM bytes = 2 x FETCH_SIZE (gfx950 reports half the bytes
-of a 16 B/lane streaming read, MI355X_MICROARCH.md "HBM / rocprofv3") +
-WRITE_SIZE, both in KB (x1024).
+roofline.traffic.  HBM bytes of a dispatch = 2 x FETCH_SIZE (gfx950 reports
+half the bytes of a 16 B/lane streaming read, MI355X_MICROARCH.md "HBM /
+rocprofv3") + WRITE_SIZE, both in KB (x1024).  The record is bytes PER ROW of
+a full-data launch (the dispatches of the selected kernel with the largest
+grid stream all n rows), so bench.py can scale it to the rows per launch of
+whatever launch mix it measured -- traffic and the algorithmic bytes then
+describe the same launches.
 
-Usage: python tools/pmc_summary.py <tag> <out-prefix> <config> <n> <p> <kernel-label> [regex]
-
-<regex> selects the dispatches of the roofline kernel (default: the config-2
-bf16 cooperative pass, irls_coop_kernel<.., 0, false, ..>).
+Usage: python tools/pmc_summary.py <tag> <out-prefix> <config> <n> <p> <kernel-key> <regex>
 """
 import csv
+import glob
 import json
 import os
 import re
 import sys
 
-tag, prefix, config, n, p, label = sys.argv[1:7]
-pattern = re.compile(sys.argv[7] if len(sys.argv) > 7 else r"irls_coop_kernel<.*, 0, false")
+tag, prefix, config, n, p, key, rx = sys.argv[1:8]
+pattern = re.compile(rx)
 root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 base = os.path.join(root, "gpurun_out", tag)
 rows = []
 for i in range(1, 5):
-    f = os.path.join(base, f"p{i}", "run_counter_collection.csv")
-    if not os.path.exists(f):
-        continue
-    for r in csv.DictReader(open(f)):
-        if any(t in r["Kernel_Name"] for t in ("irls_", "wide_", "cat_", "part_")):
-            rows.append({"pass": i, "dispatch": r["Dispatch_Id"], "kernel": r["Kernel_Name"][:120],
-                         "grid": r["Grid_Size"], "counter": r["Counter_Name"],
-                         "value": r["Counter_Value"],
-                         "ms": (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6})
+    for f in glob.glob(os.path.join(base, f"p{i}", "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if any(t in r["Kernel_Name"] for t in ("irls_", "wide_", "cat_", "part_")):
+                rows.append({"pass": i, "dispatch": r["Dispatch_Id"],
+                             "kernel": r["Kernel_Name"][:120], "grid": int(r["Grid_Size"]),
+                             "counter": r["Counter_Name"], "value": float(r["Counter_Value"]),
+                             "ms": (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6})
 out_csv = os.path.join(root, "profiles", f"{prefix}_pmc.csv")
 with open(out_csv, "w", newline="") as fh:
     w = csv.DictWriter(fh, fieldnames=list(rows[0].keys()))
     w.writeheader()
     w.writerows(rows)
 
-# bf16 (approximate) pass dispatches: the kernel template with HMODE 0
-def pick(counter):
-    return [float(r["value"]) for r in rows
-            if r["counter"] == counter and pattern.search(r["kernel"])]
-fetch, write = pick("FETCH_SIZE"), pick("WRITE_SIZE")
-assert fetch and len(fetch) == len(write), (len(fetch), len(write))
-per_launch = (2 * sum(fetch) + sum(write)) * 1024 / len(fetch)
+sel = [r for r in rows if pattern.search(r["kernel"])]
+gmax = max(r["grid"] for r in sel)
+full = [r for r in sel if r["grid"] == gmax]
+fetch = [r["value"] for r in full if r["counter"] == "FETCH_SIZE"]
+write = [r["value"] for r in full if r["counter"] == "WRITE_SIZE"]
+assert fetch and write, (len(fetch), len(write))
+per_launch = (2 * sum(fetch) / len(fetch) + sum(write) / len(write)) * 1024
 tf = os.path.join(root, "profiles", "pmc_traffic.json")
 d = json.load(open(tf)) if os.path.exists(tf) else {}
 d[f"config{config}"] = {
-    "n": int(n), "p": int(p), "kernel": label, "launches": len(fetch),
-    "hbm_bytes_per_launch": per_launch,
+    "n": int(n), "p": int(p), "kernel_key": key, "kernel": full[0]["kernel"],
+    "full_pass_launches": len(fetch),
+    "hbm_bytes_per_full_launch": per_launch,
+    "hbm_bytes_per_row": per_launch / int(n),
     "fetch_size_kb_per_launch": sum(fetch) / len(fetch),
     "write_size_kb_per_launch": sum(write) / len(write),
-    "correction": "2 x FETCH_SIZE (gfx950 half-count) + WRITE_SIZE, KB x 1024",
-    "source": f"profiles/{prefix}_pmc.csv (tools/pmc.sh, rocprofv3 --pmc, one counter group per run)",
+    "correction": "2 x FETCH_SIZE (gfx950 half-count) + WRITE_SIZE, KB x 1024; full-grid "
+                  "(all-rows) dispatches only",
+    "source": f"profiles/{prefix}_pmc.csv (tools/pmc.sh, rocprofv3 --pmc, one counter group "
+              "per run)",
 }
 json.dump(d, open(tf, "w"), indent=1)
-print(json.dumps(d, indent=1))
+print(json.dumps(d[f"config{config}"], indent=1))
