@@ -335,9 +335,48 @@ def golden_dummy():
           not np.abs(outs[4]).any())
 
 
+def golden_dummy_file():
+    """H. Dummy-level selection over a CSV file (dlsa/dummies.py:111-146):
+    the reference's select_dummy_factors_from_file on a 1.2 MB file (two
+    readlines(1024000) buffers, level frequencies drifting along the file),
+    by column names and by column positions.  The file text is rebuilt by
+    tests/golden/dummy_csv.py from its seed; only the outputs are stored."""
+    import json
+    import tempfile
+
+    import dlsa.dummies as RD  # reference
+
+    sys.path.insert(0, OUT)
+    import dummy_csv as DC
+
+    cols = DC.rows()
+    txt = DC.text(cols)
+    res = {}
+    with tempfile.TemporaryDirectory() as tmp:
+        path = os.path.join(tmp, "air.csv")
+        with open(path, "w") as fh:
+            fh.write(txt)
+        with open(path) as fh:
+            nbuf = 0
+            while fh.readlines(1024000):
+                nbuf += 1
+        for tag, dc, keep in (("names", ["Month", "UniqueCarrier", "Origin"], [1, 0.8, 0.9]),
+                              ("positions", [2, 1], [0.75, 0.95])):
+            info = RD.select_dummy_factors_from_file(path, True, dc, keep, "000_OTHERS",
+                                                     os.path.join(tmp, f"{tag}.pkl"))
+            res[tag] = info
+    np.savez_compressed(os.path.join(OUT, "dummy_file.npz"), n_buffers=nbuf, n_rows=len(txt),
+                        info_names=json.dumps(res["names"]),
+                        info_positions=json.dumps(res["positions"]))
+    print("dummy file done: buffers", nbuf)
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "dummy":
         golden_dummy()
+    elif len(sys.argv) > 1 and sys.argv[1] == "dummy_file":
+        golden_dummy_file()
     else:
         main()
         golden_dummy()
+        golden_dummy_file()

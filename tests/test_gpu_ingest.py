@@ -180,3 +180,48 @@ def test_read_csv_partitioned_unknown_level_zero_frame(torch_cuda, tmp_path, gol
         assert not missing
         r = O.logistic_fit(X, part["label"].to_numpy(float), fit_intercept=True)
         assert np.abs(fit.theta[k].cpu().numpy() - r["coef"]).max() / np.abs(r["coef"]).max() < 1e-8
+
+
+def test_csv_to_config3_fit_needs_no_reference_code(torch_cuda, tmp_path):
+    """End to end on the product alone: CSV -> dummy-level selection over the
+    file (dlsa_amd.dummies, = dummies.py:111-146) -> categorical-code HBM
+    layout (read_csv_partitioned) -> categorical fit; every partition against
+    the oracle on the reference's dense dummy design."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import dummy_csv as DC
+
+    from dlsa_amd.dummies import select_dummy_factors_from_file
+    from dlsa_amd.ingest import read_csv_partitioned, read_table
+    from dlsa_amd.models import logistic_model_batched_categorical
+
+    path = tmp_path / "air.csv"
+    path.write_text(DC.text(DC.rows()))
+    factors = ["Month", "UniqueCarrier", "Origin"]
+    info = select_dummy_factors_from_file(str(path), True, factors, [1, 0.8, 0.9], "000_OTHERS")
+    base = ["Month_1", "UniqueCarrier_000_OTHERS", "Origin_000_OTHERS"]
+    cols = factors + ["Distance"]
+    lay = read_csv_partitioned(str(path), "ArrDelay", cols, K=4, dummy_info=info,
+                               dummy_factors_baseline=base)
+    assert lay["zero_partitions"].size == 0
+    fit = logistic_model_batched_categorical(lay["Xn"], lay["codes"], lay["y"], lay["offsets"],
+                                             lay["levels"], fit_intercept=True,
+                                             center=[900.0], scale=[800.0])
+    assert (fit.status.cpu().numpy() == 0).all()
+    df = read_table(str(path), "ArrDelay", cols)
+    order, off = O.systematic_partition(np.arange(len(df)) % 4)
+    d = df.iloc[order].reset_index(drop=True)
+    for k in range(4):
+        part = d.iloc[off[k]:off[k + 1]]
+        X, names, missing = O.dummy_design({"Distance": part["Distance"].to_numpy()},
+                                           {c: part[c].to_numpy() for c in factors}, info, base)
+        assert names == lay["cols"] and not missing
+        center = np.array([900.0] + [0.0] * (X.shape[1] - 1))
+        scale = np.array([800.0] + [1.0] * (X.shape[1] - 1))
+        r = O.logistic_fit(X, part["ArrDelay"].to_numpy(float), fit_intercept=True, center=center,
+                           scale=scale)
+        assert np.abs(fit.theta[k].cpu().numpy() - r["coef"]).max() / np.abs(r["coef"]).max() < 1e-8
+        assert np.abs(fit.sig_inv[k].cpu().numpy() - r["Sig_inv"]).max() / \
+            np.abs(r["Sig_inv"]).max() < 1e-8
