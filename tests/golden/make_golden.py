@@ -371,8 +371,76 @@ def golden_dummy_file():
     print("dummy file done: buffers", nbuf)
 
 
+def golden_eval():
+    """I. The evaluation pass logistic_model_eval (models.py:151-225): per
+    partition the log-likelihood of 4 candidate coefficient columns, on
+    (a) config-1 data (p = 10) with and without intercept, (b) the same with
+    data_info standardisation, (c) the dummy branch (partitions 0-3 of the
+    dummy fixture, every level present) with intercept + data_info; and what
+    the reference does on the dummy fixture's partition 4 (a selected level
+    missing, models.py:188-195), recorded as the exception it raises."""
+    import json
+
+    rs = np.random.RandomState(23)
+    np.random.seed(2019)
+    pid, lab, feat = simulate_logistic_arrays(100000, 10, "systematic", 4)
+    cols = ["x" + str(i) for i in range(10)]
+    df = pd.DataFrame(np.concatenate([pid[:, None], lab[:, None], feat], 1),
+                      columns=["partition_id", "label"] + cols)
+    info = pd.DataFrame({"summary": ["count", "mean", "stddev", "min", "max"]})
+    for c in cols:
+        v = feat[:, cols.index(c)]
+        info[c] = [str(v.size), repr(float(v.mean() + 0.01)), repr(float(v.std(ddof=1) * 1.1)),
+                   repr(float(v.min())), repr(float(v.max()))]
+    rec = {"info": info.to_numpy().astype("U40"), "info_cols": np.array(list(info.columns), "U32")}
+    names = ["beta_byAIC", "beta_byBIC", "beta_byOLS", "beta_byONESHOT"]
+    for fi in (False, True):
+        for std in (False, True):
+            P = 10 + int(fi)
+            par = pd.DataFrame(0.6 * rs.randn(P, 4), columns=names)
+            out = []
+            for k in range(4):
+                g = df[df["partition_id"] == k].reset_index(drop=True)
+                o = RM.logistic_model_eval(g, "label", par, fit_intercept=fi,
+                                           data_info=info if std else [])
+                out.append(o.to_numpy(np.float64).reshape(-1))
+            tag = f"{'int' if fi else 'noint'}_{'std' if std else 'raw'}"
+            rec["par_" + tag] = par.to_numpy()
+            rec["ll_" + tag] = np.stack(out)
+    # dummy branch
+    gd = np.load(os.path.join(OUT, "dummy_branch.npz"))
+    ddf = pd.DataFrame({"partition_id": gd["pid"].astype(float), "label": gd["label"],
+                        "DepTime": gd["deptime"], "Distance": gd["distance"],
+                        "Month": gd["month"], "UniqueCarrier": gd["carrier"].astype(object),
+                        "Origin": gd["origin"].astype(object)})
+    dinfo = json.loads(str(gd["dummy_info"]))
+    base = [str(b) for b in gd["baseline"]]
+    dinf = pd.DataFrame(gd["info"].astype(object), columns=list(gd["info_cols"]))
+    P = len(gd["cols"]) - 3
+    par = pd.DataFrame(0.3 * rs.randn(P, 4), columns=names)
+    out = []
+    for k in range(4):
+        g = ddf[ddf["partition_id"] == k].reset_index(drop=True)
+        o = RM.logistic_model_eval(g, "label", par, fit_intercept=True, dummy_info=dinfo,
+                                   dummy_factors_baseline=base, data_info=dinf)
+        out.append(o.to_numpy(np.float64).reshape(-1))
+    rec["par_dummy"] = par.to_numpy()
+    rec["ll_dummy"] = np.stack(out)
+    g = ddf[ddf["partition_id"] == 4].reset_index(drop=True)
+    try:
+        RM.logistic_model_eval(g, "label", par, fit_intercept=True, dummy_info=dinfo,
+                               dummy_factors_baseline=base, data_info=dinf)
+        rec["missing_level_outcome"] = "returned"
+    except Exception as e:  # noqa: BLE001 - the reference's behaviour is the datum
+        rec["missing_level_outcome"] = f"raises {type(e).__name__}: {str(e)[:160]}"
+    np.savez_compressed(os.path.join(OUT, "eval.npz"), **rec)
+    print("eval done:", rec["missing_level_outcome"])
+
+
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "dummy":
+    if len(sys.argv) > 1 and sys.argv[1] == "eval":
+        golden_eval()
+    elif len(sys.argv) > 1 and sys.argv[1] == "dummy":
         golden_dummy()
     elif len(sys.argv) > 1 and sys.argv[1] == "dummy_file":
         golden_dummy_file()
@@ -380,3 +448,4 @@ if __name__ == "__main__":
         main()
         golden_dummy()
         golden_dummy_file()
+        golden_eval()

@@ -710,3 +710,67 @@ def test_nonfinite_partition_is_excluded_from_the_combine(torch_cuda, M):
     assert _rel(comb["beta_byOLS"], wlse) < REL
     assert _rel(comb["beta_byONESHOT"], oneshot) < REL
     assert _rel(comb.iloc[:, 2:].to_numpy(), Ssum) < REL
+
+
+# ---------------------------------------------------------------------------
+# evaluation pass against the reference's logistic_model_eval (eval.npz)
+# ---------------------------------------------------------------------------
+
+
+@pytest.mark.parametrize("fi", [False, True])
+@pytest.mark.parametrize("std", [False, True])
+def test_logistic_model_eval_vs_reference(golden_dir, torch_cuda, M, fi, std):
+    """models.py:151-225 with the reference's own signature and frames:
+    config-1 partitions, 4 candidate columns, intercept / data_info."""
+    import pandas as pd
+
+    from test_oracle_golden import _eval_inputs
+
+    E, pid, lab, feat, info = _eval_inputs(golden_dir)
+    tag = f"{'int' if fi else 'noint'}_{'std' if std else 'raw'}"
+    names = ["beta_byAIC", "beta_byBIC", "beta_byOLS", "beta_byONESHOT"]
+    par = pd.DataFrame(E["par_" + tag], columns=names)
+    for k in range(4):
+        m = pid == k
+        df = pd.DataFrame(np.column_stack([pid[m], lab[m], feat[m]]),
+                          columns=["partition_id", "label"] + [f"x{i}" for i in range(10)])
+        out = M.logistic_model_eval(df, "label", par, fit_intercept=fi,
+                                    data_info=info if std else [])
+        assert list(out.columns) == names and out.shape == (1, 4)
+        ref = E["ll_" + tag][k]
+        assert np.abs(out.to_numpy()[0] - ref).max() <= 1e-10 * np.abs(ref).max()
+
+
+def test_logistic_model_eval_dummy_branch_vs_reference(golden_dir, torch_cuda, M):
+    """The dummy branch of logistic_model_eval (models.py:161-205): every
+    level present (partitions 0-3 of the dummy fixture) -- the reference's
+    values; partition 4 (a selected level missing) -- the reference raises
+    (pandas 2, see test_oracle_golden), the product evaluates with that dummy
+    column = 0, checked against the oracle on that design."""
+    import pandas as pd
+
+    from test_oracle_golden import _dummy_fixture
+
+    E = np.load(os.path.join(golden_dir, "eval.npz"))
+    g, df, dinfo, base, info = _dummy_fixture(golden_dir)
+    names = ["beta_byAIC", "beta_byBIC", "beta_byOLS", "beta_byONESHOT"]
+    par = pd.DataFrame(E["par_dummy"], columns=names)
+    df = df[["partition_id", "label", "DepTime", "Distance", "Month", "UniqueCarrier", "Origin"]]
+    for k in range(4):
+        part = df[df["partition_id"] == k].reset_index(drop=True)
+        out = M.logistic_model_eval(part, "label", par, True, dinfo, base, info)
+        ref = E["ll_dummy"][k]
+        assert np.abs(out.to_numpy()[0] - ref).max() <= 1e-10 * np.abs(ref).max()
+    part = df[df["partition_id"] == 4].reset_index(drop=True)
+    with pytest.warns(UserWarning, match="missing in this data chunk"):
+        out = M.logistic_model_eval(part, "label", par, True, dinfo, base, info)
+    num = {c: part[c].to_numpy() for c in ("Distance", "DepTime")}
+    fac = {c: part[c].to_numpy() for c in ("Month", "UniqueCarrier", "Origin")}
+    X, cols, missing = O.dummy_design(num, fac, dinfo, base)
+    assert missing
+    center = np.array([float(info[c][1]) if c in num else 0.0 for c in cols])
+    scale = np.array([float(info[c][2]) if c in num else 1.0 for c in cols])
+    ref = O.logistic_loglik(X, part["label"].to_numpy(), par.to_numpy().T, fit_intercept=True,
+                            center=center, scale=scale)
+    assert np.isfinite(out.to_numpy()).all()
+    assert np.abs(out.to_numpy()[0] - ref).max() <= 1e-10 * np.abs(ref).max()
