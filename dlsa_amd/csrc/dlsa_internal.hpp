@@ -18,6 +18,13 @@ enum : int32_t { PHASE_F32 = 0, PHASE_F64 = 1, PHASE_DONE = 2, PHASE_LEVEL_DONE 
 enum : int32_t { STATUS_RUNNING = -1 };
 enum : int32_t { FAMILY_LOGISTIC = 0, FAMILY_GAUSSIAN = 1 };
 
+// Cache policy of the LDS-DMA loads that stream X (the aux / cpol operand of
+// buffer_load ... lds): X is read once per pass and is far larger than every
+// cache, so streaming it non-temporally (2 = nt) is the default candidate;
+// profiling builds override it (tools/build_variants.sh).
+#ifndef DLSA_X_DMA_AUX
+#define DLSA_X_DMA_AUX 0
+#endif
 // Cooperative pass: 4 (8) waves per workgroup, 32-row blocks.
 constexpr int kCoopRows = 32;
 // MFMA arithmetic of a pass's Hessian.

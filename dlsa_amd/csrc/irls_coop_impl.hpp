@@ -376,7 +376,8 @@ void irls_coop_kernel(const PassArgs a) {
       int j = wid + W * i;
       const int jj = j < npieces ? j : npieces - 1;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          xr_rsrc, (lds_void_t*)(sbase + G::PAD + jj * 1024), 16, vx, so + jj * 1024, 0, 0);
+          xr_rsrc, (lds_void_t*)(sbase + G::PAD + jj * 1024), 16, vx, so + jj * 1024, 0,
+          DLSA_X_DMA_AUX);
     }
     __builtin_amdgcn_raw_ptr_buffer_load_lds(yr_rsrc, (lds_void_t*)(sbase + slot_x), 4, vy,
                                              bb * RB * 8, 0, 0);

@@ -288,7 +288,7 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
     const int so = __builtin_amdgcn_readfirstlane((int)((start & ~(uintptr_t)15) - cx.xcb));
     for (int j = WID; j < cx.npieces; j += W)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(cx.xr, (wlds_void_t*)(sbase + 16 + j * 1024), 16,
-                                               lane * 16, so + j * 1024, 0, 0);
+                                               lane * 16, so + j * 1024, 0, DLSA_X_DMA_AUX);
     if (WID == W - 1)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(cx.yr, (wlds_void_t*)(sbase + cx.slot_y), 4,
                                                lane * 4, blk * RB * 8, 0, 0);

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Profiling-only builds of libdlsa_hip.so with DLSA_ABLATE=1/2/3 (see
-# dlsa_amd/csrc/irls_pass.hip and irls_coop.hip).  Output: tools/_variants/*.so (git-ignored).
+# dlsa_amd/csrc/irls_coop_impl.hpp; nt / sc1: cache policy of the X stream).  Output: tools/_variants/*.so (git-ignored).
 set -e
 mkdir -p tools/_variants
 cd "$(dirname "$0")/.."
@@ -18,6 +18,8 @@ for v in "$@"; do
     cat16) D=DLSA_CAT_ABLATE=16 ;;
     solveprof) D=DLSA_SOLVE_PROFILE=1 ;;
     cat31) D=DLSA_CAT_ABLATE=31 ;;
+    nt) D=DLSA_X_DMA_AUX=2 ;;
+    sc1) D=DLSA_X_DMA_AUX=1 ;;
     *) echo "unknown variant $v"; exit 1 ;;
   esac
   python -c "from dlsa_amd.build import build; print(build(force=True, out='tools/_variants/libdlsa_hip_$v.so', defines=['$D']))"

@@ -1,6 +1,7 @@
 """Summarise a tools/pmc.sh run into profiles/.
 
-Reads gpurun_out/<tag>/p{1..4}/**/*counter_collection.csv, writes
+Reads gpurun_out/<tag>/<run>/**/*counter_collection.csv (one counter
+group per run directory), writes
 profiles/<prefix>_pmc.csv (per-dispatch counters of the pass kernels) and
 updates profiles/pmc_traffic.json, the file bench.py reads for
 roofline.traffic.  HBM bytes of a dispatch = 2 x FETCH_SIZE (gfx950 reports
@@ -25,14 +26,14 @@ pattern = re.compile(rx)
 root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 base = os.path.join(root, "gpurun_out", tag)
 rows = []
-for i in range(1, 5):
-    for f in glob.glob(os.path.join(base, f"p{i}", "**", "*counter_collection.csv"), recursive=True):
-        for r in csv.DictReader(open(f)):
-            if any(t in r["Kernel_Name"] for t in ("irls_", "wide_", "cat_", "part_")):
-                rows.append({"pass": i, "dispatch": r["Dispatch_Id"],
-                             "kernel": r["Kernel_Name"][:120], "grid": int(r["Grid_Size"]),
-                             "counter": r["Counter_Name"], "value": float(r["Counter_Value"]),
-                             "ms": (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6})
+for f in sorted(glob.glob(os.path.join(base, "**", "*counter_collection.csv"), recursive=True)):
+    i = os.path.relpath(f, base).split(os.sep)[0]  # one counter group per run directory
+    for r in csv.DictReader(open(f)):
+        if any(t in r["Kernel_Name"] for t in ("irls_", "wide_", "cat_", "part_")):
+            rows.append({"pass": i, "dispatch": r["Dispatch_Id"],
+                         "kernel": r["Kernel_Name"][:120], "grid": int(r["Grid_Size"]),
+                         "counter": r["Counter_Name"], "value": float(r["Counter_Value"]),
+                         "ms": (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6})
 out_csv = os.path.join(root, "profiles", f"{prefix}_pmc.csv")
 with open(out_csv, "w", newline="") as fh:
     w = csv.DictWriter(fh, fieldnames=list(rows[0].keys()))
