@@ -172,7 +172,8 @@ def main():
     ap.add_argument("--partitions", type=int, default=0)
     ap.add_argument("--hessian", default="mixed", choices=["mixed", "fp64", "mixed_f32"])
     ap.add_argument("--tol", type=float, default=1e-10)
-    ap.add_argument("--cpu-parts", type=int, default=32)
+    ap.add_argument("--cpu-parts", type=int, default=0,
+                    help="partitions of the CPU baseline sample (0: ~10-30 s of CPU work per config)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--seed", type=int, default=2019)
@@ -396,7 +397,10 @@ def main():
     if os.path.exists(pmc_file):
         try:
             rec = json.load(open(pmc_file)).get(f"config{args.config}", {})
-            if rec.get("p") == p and rec.get("kernel_key") == pmc_key:
+            if rec.get("p") == p and rec.get("kernel_key") == pmc_key and \
+                    rec.get("calibrated", True) is False:
+                roof["traffic_note"] = rec.get("note")
+            elif rec.get("p") == p and rec.get("kernel_key") == pmc_key:
                 roof["traffic"] = rec["hbm_bytes_per_row"] * roof["rows_per_launch"]
                 roof["traffic_bytes_per_row"] = rec["hbm_bytes_per_row"]
                 roof["algorithmic_bytes_per_row"] = row_bytes
@@ -447,8 +451,9 @@ def main():
         workers = min(16, os.cpu_count() or 1)
         if args.config == 5:
             nk_cpu, parts = 20000, 16      # ~8 s of single-thread work per partition
-        else:
-            nk_cpu, parts = n // K, args.cpu_parts
+        else:                              # ~10-30 s of single-thread work in all
+            nk_cpu, parts = n // K, {2: 32, 3: 32, 4: 128}[args.config]
+        parts = args.cpu_parts or parts
         out["cpu_baseline"] = cpu_baseline(nk_cpu, p, parts, workers, family, data=data)
         out["vs_cpu_baseline"] = value / out["cpu_baseline"]["value"]
     if rank == 0:

@@ -9,12 +9,15 @@ LIBS=${2:-base}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
+if [ "$LIBS" != none ]; then
 echo "[meas] $(date +%T) pass A/B ($LIBS)" &&
 timeout -k 10 300 python -u tools/pass_bench.py --n 50000000 --p 100 --K 512 --rounds 3 \
     --libs "$LIBS" > "$OUT/pass_mixed.jsonl" 2> "$OUT/pass_mixed.err" && cat "$OUT/pass_mixed.jsonl" &&
 timeout -k 10 300 python -u tools/pass_bench.py --n 25000000 --p 100 --K 256 --rounds 3 --hessian fp64 \
     --libs "$LIBS" > "$OUT/pass_fp64.jsonl" 2> "$OUT/pass_fp64.err" && cat "$OUT/pass_fp64.jsonl" || exit $?
+fi
 for c in 2 3 4 5; do
+  mkdir -p "$OUT/pmc_c$c"
   for grp in FETCH_SIZE WRITE_SIZE; do
     echo "[meas] $(date +%T) pmc config $c $grp"
     timeout -s KILL 180 rocprofv3 --pmc $grp --output-format csv -d "$OUT/pmc_c$c/$grp" -o run -- \

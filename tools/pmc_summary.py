@@ -41,8 +41,11 @@ with open(out_csv, "w", newline="") as fh:
     w.writerows(rows)
 
 sel = [r for r in rows if pattern.search(r["kernel"])]
+# the full-data launches: the largest grid and, among those, the long
+# dispatches (a warm-start level can keep the grid but stream 1/16 of the rows)
 gmax = max(r["grid"] for r in sel)
-full = [r for r in sel if r["grid"] == gmax]
+tmax = max(r["ms"] for r in sel if r["grid"] == gmax)
+full = [r for r in sel if r["grid"] == gmax and r["ms"] >= 0.7 * tmax]
 fetch = [r["value"] for r in full if r["counter"] == "FETCH_SIZE"]
 write = [r["value"] for r in full if r["counter"] == "WRITE_SIZE"]
 assert fetch and write, (len(fetch), len(write))
@@ -56,8 +59,8 @@ d[f"config{config}"] = {
     "hbm_bytes_per_row": per_launch / int(n),
     "fetch_size_kb_per_launch": sum(fetch) / len(fetch),
     "write_size_kb_per_launch": sum(write) / len(write),
-    "correction": "2 x FETCH_SIZE (gfx950 half-count) + WRITE_SIZE, KB x 1024; full-grid "
-                  "(all-rows) dispatches only",
+    "correction": "2 x FETCH_SIZE (gfx950 half-count) + WRITE_SIZE, KB x 1024; full-data "
+                  "dispatches only (largest grid, >= 0.7 x the longest)",
     "source": f"profiles/{prefix}_pmc.csv (tools/pmc.sh, rocprofv3 --pmc, one counter group "
               "per run)",
 }
