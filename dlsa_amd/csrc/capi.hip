@@ -188,9 +188,9 @@ struct WidePlans {
   Plan rows, gram;
 };
 
-// Row pass: ~2048 chunks (one 256-thread workgroup each, HBM-bound).  Gram
-// pass: ~1024 (row group, tile) workgroups, a multiple of 8 row groups so the
-// XCD-aware mapping fills every XCD.
+// Row pass (exact partitions): ~2048 chunks (one 256-thread workgroup each,
+// HBM-bound).  Gram row groups (fused bf16 pass and fp64 Gram pass): >= 256,
+// a multiple of 8 so the XCD-aware mappings fill every XCD.
 static void make_wide_plans(const int64_t* offsets, int K, int p, int intercept,
                             int rows_per_chunk, WidePlans& wp, double frac = 1.0,
                             int64_t min_rows = 0) {
@@ -201,12 +201,11 @@ static void make_wide_plans(const int64_t* offsets, int K, int p, int intercept,
   const int NB = (P + kWideTile - 1) / kWideTile;
   const int TB = NB * (NB + 1) / 2;
   int rpc_row = (int)std::max<int64_t>(256, std::min<int64_t>(n_total / 2048, 16384));
-  // >= 256 row groups: the all-tiles bf16 Gram pass runs wide_gram_all_groups(NB)
-  // workgroups per row group (4 at P > 384: 1024 in all) and the fp64 tiled
-  // pass TB per row group; measured at config 5 (p = 500): 64 / 128 / 256 row
-  // groups -> 183 / 188 / 177 ms per fit (fp64 pass 43.8 / 36.8 / 36.1 ms)
-  int64_t groups = (std::max<int64_t>(256, (1024 + TB - 1) / TB) + 7) / 8 * 8;
-  if (getenv("DLSA_WIDE_GRAM_TILED")) groups = ((1024 + TB - 1) / TB + 7) / 8 * 8;
+  // >= 256 row groups: the fused pass runs 2 workgroups per row group above
+  // PP = 256 (512 in all, 1 per CU), the fp64 Gram pass TB per row group;
+  // measured at config 5 (p = 500), fp64 pass: 64 / 128 / 256 row groups ->
+  // 43.8 / 36.8 / 36.1 ms
+  const int64_t groups = (std::max<int64_t>(256, (1024 + TB - 1) / TB) + 7) / 8 * 8;
   int rpc_gram = (int)std::max<int64_t>(1024, std::min<int64_t>((n_total + groups - 1) / groups,
                                                                 int64_t(1) << 24));
   if (rows_per_chunk > 0) rpc_row = rpc_gram = rows_per_chunk;
@@ -218,7 +217,7 @@ static void make_wide_plans(const int64_t* offsets, int K, int p, int intercept,
 struct WideLayout {
   int64_t off_r_row0, off_r_rows, off_r_part, off_rcb;
   int64_t off_g_row0, off_g_rows, off_g_part, off_gcb;
-  int64_t off_offsets, off_w, off_slabg, off_slabll, off_slabG, off_H;
+  int64_t off_offsets, off_w, off_slabg, off_slabll, off_slabG, off_slabgz, off_slabllz, off_H;
   int64_t off_phase, off_bt, off_llprev, off_thprev, off_dprev, off_counters;
   int64_t total;
   int64_t cap_rows, cap_gram;  // row-chunk / Gram-row-group capacity of the tables and slabs
@@ -258,6 +257,8 @@ static WideLayout make_wide_layout(const std::vector<WidePlans>& plans, int K, i
   L.off_slabg = take(8 * nr * PP);
   L.off_slabll = take(8 * nr);
   L.off_slabG = take(8 * ng * TB * kWideTile * kWideTile);
+  L.off_slabgz = take(8 * ng * PP);
+  L.off_slabllz = take(8 * ng);
   L.off_H = take(8LL * K * PP * PP);
   L.off_phase = take(4LL * K);
   L.off_bt = take(4LL * K);
@@ -447,9 +448,10 @@ struct StreamTimer {
   }
 };
 
-// P > DLSA_MAX_P_FUSED (wide_pass.hip): per Newton iteration a row pass, a
-// Gram pass per running precision phase, the deterministic partial-tile
-// assembly and the per-partition blocked-Cholesky update.  Same warm-start
+// P > DLSA_MAX_P_FUSED (wide_pass.hip): per Newton iteration the fused bf16
+// pass (PHASE_F32 partitions) and/or the row + fp64 Gram passes (PHASE_F64),
+// the deterministic partial-tile assembly and the per-partition
+// blocked-Cholesky update.  Same warm-start
 // levels, phases, state machine and outputs as the fused path.
 static int fit_wide(int family, const double* X, const double* y, const int64_t* offsets,
                     int32_t K, int32_t p, int32_t fit_intercept, const double* center,
@@ -511,6 +513,8 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
   wa.slab_g = (double*)at(L.off_slabg);
   wa.slab_ll = (double*)at(L.off_slabll);
   wa.slab_G = (double*)at(L.off_slabG);
+  wa.slab_gz = (double*)at(L.off_slabgz);
+  wa.slab_llz = (double*)at(L.off_slabllz);
   wa.p = p;
   wa.P = P;
   wa.intercept = fit_intercept ? 1 : 0;
@@ -609,29 +613,30 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
     // with full-row passes and a published Sig_inv)
     const int it_end = it + (final_level ? max_iter : kLevelIters);
     for (; it < it_end && (n_running[0] + n_running[1]) > 0 && q.rows.n_chunks > 0; ++it) {
-      DLSA_HIP_TRY(timed(&g_stats.ms_wide_row, [&] {
-        return launch_wide_row(wa, standardize, family, q.rows.n_chunks, stream);
-      }));
-      for (int ph = 0; ph < 2; ++ph) {
-        if (n_running[ph] == 0) continue;
-        wa.want_phase = ph;
+      // approximate partitions: one fused pass (gradient + bf16 Hessian)
+      if (n_running[PHASE_F32] > 0) {
         DLSA_HIP_TRY(timed(
-            &g_stats.ms_wide_gram,
-            [&] { return launch_wide_gram(wa, standardize, ph == PHASE_F64, stream); },
-            ph == PHASE_F64 ? &g_stats.ms_pass_fp64 : &g_stats.ms_pass_fp32));
-        if (ph == PHASE_F64) {
-          g_stats.passes_fp64++;
-          g_stats.rows_fp64 += phase_rows(part_rows, h_phase, ph);
-        } else {
-          g_stats.passes_fp32++;
-          g_stats.rows_fp32 += phase_rows(part_rows, h_phase, ph);
-        }
+            &g_stats.ms_wide_gram, [&] { return launch_wide_fused(wa, standardize, stream); },
+            &g_stats.ms_pass_fp32));
+        g_stats.passes_fp32++;
+        g_stats.rows_fp32 += phase_rows(part_rows, h_phase, PHASE_F32);
+      }
+      // exact partitions: row pass (gradient, w) + fp64 Gram pass
+      if (n_running[PHASE_F64] > 0) {
+        DLSA_HIP_TRY(timed(&g_stats.ms_wide_row, [&] {
+          return launch_wide_row(wa, standardize, family, q.rows.n_chunks, stream);
+        }));
+        DLSA_HIP_TRY(timed(
+            &g_stats.ms_wide_gram, [&] { return launch_wide_gram(wa, standardize, stream); },
+            &g_stats.ms_pass_fp64));
+        g_stats.passes_fp64++;
+        g_stats.rows_fp64 += phase_rows(part_rows, h_phase, PHASE_F64);
       }
       DLSA_HIP_TRY(timed(&g_stats.ms_wide_assemble,
                          [&] { return launch_wide_assemble(wa, d_gcb, d_H, K, stream); }));
       DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
       DLSA_HIP_TRY(timed(&g_stats.ms_solve,
-                         [&] { return launch_wide_newton(sa, wa, d_rcb, d_H, K, stream); }));
+                         [&] { return launch_wide_newton(sa, wa, d_rcb, d_gcb, d_H, K, stream); }));
       DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, stream));
       DLSA_HIP_TRY(hipMemcpyAsync(h_phase.data(), d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
       DLSA_HIP_TRY(hipStreamSynchronize(stream));

@@ -118,9 +118,10 @@ struct WideArgs {
   double* slab_g;          // [n_rchunks, PP] partial gradients
   double* slab_ll;         // [n_rchunks] partial log-likelihoods
   double* slab_G;          // [n_gchunks, TB, 128 * 128] partial Gram tiles
+  double* slab_gz;         // [n_gchunks, PP] fused pass: partial gradients
+  double* slab_llz;        // [n_gchunks] fused pass: partial log-likelihoods
   int32_t p, P, intercept;
   int32_t NB;              // 128-wide column blocks, PP = 128 NB
-  int32_t want_phase;      // Gram pass: partitions in this phase
   int32_t n_gchunks;
 };
 
@@ -179,13 +180,12 @@ hipError_t launch_cat_mark(const CatArgs& a, const int32_t* pcb, const int32_t* 
                            int32_t* bad_part, hipStream_t s);
 hipError_t launch_wide_row(const WideArgs& a, bool standardize, int family, int n_chunks,
                            hipStream_t s);
-hipError_t launch_wide_gram(const WideArgs& a, bool standardize, bool f64, hipStream_t s);
-hipError_t launch_wide_gram_all(const WideArgs& a, bool standardize, hipStream_t s);
-int wide_gram_all_groups(int NB);  // workgroups per row group of the all-tiles bf16 pass
+hipError_t launch_wide_gram(const WideArgs& a, bool standardize, hipStream_t s);
+hipError_t launch_wide_fused(const WideArgs& a, bool standardize, hipStream_t s);
 hipError_t launch_wide_assemble(const WideArgs& a, const int32_t* gcb, double* Hfull, int K,
                                 hipStream_t s);
 hipError_t launch_wide_newton(const SolveArgs& sa, const WideArgs& wa, const int32_t* rcb,
-                              double* Hfull, int K, hipStream_t s);
+                              const int32_t* gcb, double* Hfull, int K, hipStream_t s);
 int wide_newton_lds_bytes(int NB);
 hipError_t launch_loglik_eval(const EvalArgs& a, int n_chunks, hipStream_t s);
 hipError_t launch_loglik_reduce(const double* partial, const int32_t* pcb, int K, int B,

@@ -3,17 +3,21 @@
 // logistic_LBFGS_local.py:12-13).  Same per-partition contract as the fused
 // pass (dlsa/models.py:110-131: MLE theta_k, Sig_inv_k = X_k^T W X_k at
 // theta_k), but the P x P Hessian no longer fits a workgroup's registers and
-// LDS, so one Newton iteration is split into four launches:
+// LDS, so one Newton iteration is split into launches:
 //
-//   wide_row_kernel     one streaming pass over X (HBM-bound): eta = x.theta,
-//                       mu, w = mu(1-mu), gradient X^T (y - mu), log-lik;
+//   wide_fused_bf16_kernel  PHASE_F32 partitions (MIXED mode): ONE stream of X
+//                       gives eta, w, the fp64 gradient / log-lik AND the
+//                       approximate Hessian Z^T Z, Z = bf16(sqrt(w) x)
+//                       (bf16 MFMA 16x16x32, fp32 accumulation).
+//   wide_row_kernel     PHASE_F64 partitions: one streaming pass over X
+//                       (HBM-bound): eta, mu, w = mu(1-mu), gradient, log-lik;
 //                       writes w[row] (8 B/row) and per-chunk partials.
-//   wide_gram_kernel    X^T diag(w) X as 128x128 lower-triangle output tiles,
-//                       split over row groups (fp64 MFMA 16x16x4, MFMA-bound).
-//                       blockIdx -> (row group, tile) is XCD-aware: all tiles
-//                       of a row group run on one XCD, so its rows are
-//                       fetched from HBM once and re-read from that XCD's L2
-//                       / the MALL.
+//   wide_gram_kernel    PHASE_F64: X^T diag(w) X as 128x128 lower-triangle
+//                       output tiles, split over row groups (fp64 MFMA
+//                       16x16x4, MFMA-bound).  blockIdx -> (row group, tile)
+//                       is XCD-aware: all tiles of a row group run on one XCD,
+//                       so its rows are fetched from HBM once and re-read from
+//                       that XCD's L2 / the MALL.
 //   wide_assemble_kernel  fixed-order sum of the row-group partials into the
 //                       padded PP x PP Hessian of each partition (identity on
 //                       the padding) -- deterministic.
@@ -27,6 +31,7 @@
 #include <stdlib.h>
 
 #include "dlsa_internal.hpp"
+#include "irls_wave_impl.hpp"  // wv_* wave helpers
 
 namespace dlsa {
 
@@ -76,8 +81,7 @@ template <int MB, bool STD, int FAM>
 __global__ __launch_bounds__(256) void wide_row_kernel(const WideArgs a) {
   const int chunk = blockIdx.x;
   const int part = a.rc_part[chunk];
-  const int ph = a.phase[part];
-  if (ph != PHASE_F32 && ph != PHASE_F64) return;  // workgroup-uniform
+  if (a.phase[part] != PHASE_F64) return;  // workgroup-uniform (PHASE_F32: fused pass)
   __shared__ double red[4 * 64 * MB + 4];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int p = a.p, P = a.P, ic = a.intercept;
@@ -179,7 +183,7 @@ __global__ __launch_bounds__(512, 1) void wide_gram_kernel(const WideArgs a) {
   const int chunk = cl * 8 + xcd;  // all TB tiles of a row group on one XCD
   if (chunk >= a.n_gchunks) return;
   const int part = a.gc_part[chunk];
-  if (a.phase[part] != a.want_phase) return;
+  if (a.phase[part] != PHASE_F64) return;
   int I, J;
   tile_ij(t, I, J);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -301,341 +305,453 @@ __global__ __launch_bounds__(512, 1) void wide_gram_kernel(const WideArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// approximate Gram pass (bf16 MFMA, fp32 accumulation) for the Newton steps
-// before the fp64 pass (the approximate Hessian only steers
-// Newton; the fp64 gradient fixes the solution).  Same (row group, tile)
-// grid and XCD mapping as wide_gram_kernel.  Per 32-row block the 512
-// threads stage the tile's two 128-feature column blocks through LDS:
-// thread (feature f = t & 127, row octet g = t >> 7) loads rows 8g .. 8g+7
-// of feature f (each load instruction = 64 consecutive features of one row,
-// 512 contiguous bytes), converts to bf16 (A image: w x, B image: x) and
-// writes the 8 rows as ONE 16-byte LDS store -- exactly the k-contiguous
-// operand of v_mfma_f32_16x16x32_bf16 (lane (i, kg) reads feature i, rows
-// 8 kg .. 8 kg + 7 with one ds_read_b128).  Feature stride 80 B: the 16
-// lanes of an operand read hit 16 distinct 16-byte bank groups.
-// Double-buffered images: one barrier per block.
+// fused approximate pass (MIXED mode, logistic, PHASE_F32 partitions): ONE
+// stream of X per Newton iteration yields both the row quantities (eta, w, r,
+// the fp64 gradient X^T (y - mu) and log-likelihood) and the approximate
+// Hessian  H~ = Z^T Z,  Z = bf16(sqrt(w) x)  (positive semi-definite by
+// construction; DESIGN.md 4.2: it only steers Newton, the fp64 pass fixes the
+// solution and publishes Sig_inv).
+//
+// Register budget first: the fp32 accumulators of the P x P lower triangle
+// (528 16x16 tiles = 528 KB at PP = 512) exceed a CU's register file, so
+// S = 2 workgroups share a row group above PP = 256, each owning half of the
+// tile rows; they are dispatched back to back onto one XCD, so the second
+// stream of the rows is an L2 / MALL hit.  A workgroup is 4 waves, ONE per
+// SIMD, so each wave has the full 512 registers: ~256 accumulator registers
+// (AGPRs) + a 32-row block of X in flight (128 VGPRs) + the row work.
+//
+// Per 32-row block (wave w holds rows 8w .. 8w+7 in registers; raw buffer
+// loads, 16 B per lane at even p: lane l owns columns 2l + 128 j (+1); rows or
+// columns past the end read as 0 through the buffer range check):
+//   1. eta of the 8 rows: lane partials, then a reduce-scatter over the lanes
+//      (permlane32 / permlane16 swaps, one DPP swap, DPP within 8 lanes) --
+//      lane group l >> 3 ends with row l >> 3, bitwise-identical in the group;
+//   2. w, r, log-lik: ONE fp64 exp / reciprocal sequence for the 8 rows,
+//      broadcast by readlane; the softplus sum is a running product
+//      (frexp-normalised), one log per lane at the end;
+//   3. gradient FMAs (group 0 only) and the Z image of the block in LDS:
+//      feature-major [PP][32 rows] bf16, 80-byte feature stride (the 16 lanes
+//      of an MFMA operand read hit 16 distinct bank groups), one
+//      ds_write_b128 per (lane, column) = the wave's 8 rows of that feature;
+//   4. the loads of block b+1 are issued into the same registers, one LDS
+//      barrier (no vmcnt drain), and the MFMA phase: v_mfma_f32_16x16x32_bf16
+//      with operand lane (i, kg) = feature i, rows 8 kg .. 8 kg + 7 (one
+//      ds_read_b128) -- the loads stay in flight behind it.
+// Wave slot s = 4 sg + w owns the tile-row pairs q = s + 4 S k: rows q and
+// NT16 - 1 - q, NT16 + 1 tiles per pair (2 pairs = 66 tiles at PP = 512).
+// Double-buffered Z images: one barrier per block.  Output: the
+// 128 x 128-tile slab layout of wide_gram_kernel (slab_G) and per-row-group
+// gradient / log-lik partials (slab_gz / slab_llz) summed in fixed order --
+// deterministic.
 // ---------------------------------------------------------------------------
 typedef __bf16 bf16x8w __attribute__((ext_vector_type(8)));
 typedef float f4w __attribute__((ext_vector_type(4)));
+typedef double d2w __attribute__((ext_vector_type(2)));
 
 namespace {
-constexpr int IMG_STRIDE = 80;                       // bytes per feature row of an image
-constexpr int IMG_BYTES = GT * IMG_STRIDE;           // one 128-feature x 32-row image
-}  // namespace
-
-template <bool STD>
-__global__ __launch_bounds__(512, 1) void wide_gram_bf16_kernel(const WideArgs a) {
-  __shared__ __attribute__((aligned(16))) char img[2][2][IMG_BYTES];  // [buf][A | B]
-  const int NB = a.NB;
-  const int TB = NB * (NB + 1) / 2;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, j8 = bid >> 3;
-  const int cl = j8 / TB, t = j8 - cl * TB;
-  const int chunk = cl * 8 + xcd;
-  if (chunk >= a.n_gchunks) return;
-  const int part = a.gc_part[chunk];
-  if (a.phase[part] != a.want_phase) return;  // workgroup-uniform
-  int I, J;
-  tile_ij(t, I, J);
-  const bool diag = I == J;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int qi = wid >> 1, qj = wid & 1;
-  const bool mma = !(diag && qj == 1 && qi < 2);  // wave-uniform
-  const int p = a.p, ic = a.intercept;
-  const int64_t row0 = a.gc_row0[chunk];
-  const int nrows = a.gc_rows[chunk];
-  const int nb = (nrows + 31) / 32;
-
-  // staging role: feature fs of both column blocks, rows 8 g .. 8 g + 7
-  const int fs = tid & 127, g = tid >> 7;
-  auto feat = [&](int blk, int& col, bool& in, bool& one, double& c, double& s) {
-    const int f = GT * blk + fs, jj = f - ic;
-    in = jj >= 0 && jj < p;
-    one = ic && f == 0;
-    col = in ? jj : 0;
-    c = 0.0;
-    s = 1.0;
-    if constexpr (STD) {
-      if (in) {
-        c = a.center[jj];
-        s = 1.0 / a.scale[jj];
-      }
-    }
-  };
-  int colI, colJ;
-  bool inI, inJ, oneI, oneJ;
-  double cI, sI, cJ, sJ;
-  feat(I, colI, inI, oneI, cI, sI);
-  feat(J, colJ, inJ, oneJ, cJ, sJ);
-
-  double xi[8], xj[8], wv[8];
-  auto load = [&](int b) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int r = 32 * b + 8 * g + e;
-      const bool valid = r < nrows;
-      const int rc = valid ? r : nrows - 1;
-      const double* xr = a.X + (row0 + rc) * (int64_t)p;
-      wv[e] = valid ? a.w[row0 + rc] : 0.0;
-      xi[e] = xr[colI];
-      if (!diag) xj[e] = xr[colJ];
-    }
-  };
-  auto stage = [&](int buf) {
-    bf16x8w va, vb;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      double v = inI ? xi[e] : 0.0;
-      if constexpr (STD) v = (v - cI) * sI;
-      if (oneI) v = 1.0;
-      va[e] = (__bf16)(float)(v * wv[e]);
-      double u = v;
-      if (!diag) {
-        u = inJ ? xj[e] : 0.0;
-        if constexpr (STD) u = (u - cJ) * sJ;
-        if (oneJ) u = 1.0;
-      }
-      vb[e] = (__bf16)(float)u;
-    }
-    *(bf16x8w*)(img[buf][0] + fs * IMG_STRIDE + 16 * g) = va;
-    *(bf16x8w*)(img[buf][1] + fs * IMG_STRIDE + 16 * g) = vb;
-  };
-
-  f4w acc[2][4];
-#pragma unroll
-  for (int s = 0; s < 2; ++s)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[s][b] = f4w{0.f, 0.f, 0.f, 0.f};
-  const int fl = lane & 15, kg = lane >> 4;
-
-  if (nb > 0) {
-    load(0);
-    stage(0);
-  }
-  for (int b = 0; b < nb; ++b) {
-    if (b + 1 < nb) load(b + 1);  // in flight during the barrier and the MFMAs
-    __syncthreads();              // image b % 2 complete; image (b+1) % 2 free
-    if (mma) {
-      const char* A = img[b & 1][0];
-      const char* B = img[b & 1][1];
-      bf16x8w av[2], bv[4];
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-        av[s] = *(const bf16x8w*)(A + (32 * qi + 16 * s + fl) * IMG_STRIDE + 16 * kg);
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        bv[c] = *(const bf16x8w*)(B + (64 * qj + 16 * c + fl) * IMG_STRIDE + 16 * kg);
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          acc[s][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[s], bv[c], acc[s][c], 0, 0, 0);
-    }
-    if (b + 1 < nb) stage((b + 1) & 1);
-  }
-
-  if (!mma) return;
-  // C/D map of the f32 16x16 MFMAs: row = 4 (l >> 4) + r, column = l & 15
-  double* G = a.slab_G + ((int64_t)chunk * TB + t) * (GT * GT);
-#pragma unroll
-  for (int s = 0; s < 2; ++s)
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = 32 * qi + 16 * s + 4 * kg + r;
-        const int jc = 64 * qj + 16 * c + fl;
-        G[i * GT + jc] = (double)acc[s][c][r];
-      }
+constexpr int FZ = 80;  // bytes per feature of a Z image: 32 rows of bf16 + 16 B pad
+constexpr int FW = 4;   // waves per workgroup of the fused pass
+__host__ __device__ constexpr int fused_groups(int NT16) { return NT16 > 16 ? 2 : 1; }
+__host__ __device__ constexpr int fused_pairs_per_slot(int NT16) {
+  return (NT16 / 2 + FW * fused_groups(NT16) - 1) / (FW * fused_groups(NT16));
+}
+// [2][PP][FZ] Z images, [PP] scaled beta, [2][PP] 1/scale and center/scale,
+// [FW][PP] gradient reduction, [32] misc
+__host__ __device__ constexpr int fused_lds_bytes(int NT16) {
+  return 2 * 16 * NT16 * FZ + (3 + FW) * 16 * NT16 * 8 + 256;
 }
 
+// Sum over the 64 lanes; every lane ends with the bitwise-identical total
+// (each step adds a value and its partner's under a lane involution, so the
+// pair computes a + b and b + a).
+__device__ __forceinline__ double wave_allsum(double v) {
+  v += wv_dpp<0x141>(v);  // row_half_mirror: i <-> 7 - i
+  v += wv_dpp<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+  v += wv_dpp<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+  v += wv_dpp<0x140>(v);  // row_mirror: i <-> 15 - i
+  v = wv_xor16(v);
+  v = wv_xor32(v);
+  return v;
+}
 
-// ---------------------------------------------------------------------------
-// bf16 Gram pass, one pass over a row group for ALL its tiles (approximate
-// Hessian of the MIXED mode).  The per-tile kernel above re-reads each row
-// once per 128 x 128 tile that needs it (5x at P = 500: L2/MALL-bound, 16 ms
-// per pass at config 5); here a workgroup streams its rows once:
-//   Z = bf16(sqrt(w) x),  H~ = Z^T Z   (positive semi-definite by construction)
-// per 32-row block: 512 threads load x (fp64, coalesced along the features),
-// scale, convert and write the feature-major image Z[PP][32] (96-byte feature
-// stride: conflict-free ds_read_b128 operand reads), one barrier, then each
-// wave runs one v_mfma_f32_16x16x32_bf16 per owned 16 x 16 lower-triangle
-// tile.  The fp32 accumulators of all NT16 (NT16 + 1) / 2 tiles must fit the
-// workgroup's registers: S workgroups share a row group, each owning a
-// contiguous range of the tiles (S = 2 / 4 above PP = 256 / 384; they run on
-// one XCD, so the repeated reads of the rows are L2 hits).  Output: the 128 x 128-tile
-// slab layout of wide_gram_kernel (wide_assemble_kernel reads the lower
-// triangle of diagonal tiles only).
-// ---------------------------------------------------------------------------
-namespace {
-constexpr int ZS = 96;  // bytes per feature row of the Z image (32 rows of bf16 + pad)
-// 16x16 tiles of the lower triangle: 136 / 300 / 528 at NT16 = 16 / 24 / 32;
-// the accumulators of a group (4 VGPRs per tile per wave) stay <= ~150 VGPRs
-__host__ __device__ constexpr int zall_groups(int NT16) {
-  return NT16 > 24 ? 4 : (NT16 > 16 ? 2 : 1);
+// v_permlane32_swap / v_permlane16_swap of a double pair (a, b): after the
+// swap, lanes of the lower half of each 2H-lane group see (a, a of lane + H),
+// lanes of the upper half (b of lane - H, b)
+template <int H>
+__device__ __forceinline__ double swap_add(double a, double b) {
+  const unsigned alo = __double2loint(a), ahi = __double2hiint(a);
+  const unsigned blo = __double2loint(b), bhi = __double2hiint(b);
+  if constexpr (H == 32) {
+    const auto lo = __builtin_amdgcn_permlane32_swap(alo, blo, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap(ahi, bhi, false, false);
+    return __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+  } else {
+    const auto lo = __builtin_amdgcn_permlane16_swap(alo, blo, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap(ahi, bhi, false, false);
+    return __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+  }
+}
+
+// 8 row partials per lane -> lane l holds the total of row l >> 3 (every lane
+// of the 8-lane group bitwise-identical)
+__device__ __forceinline__ double reduce_scatter8(const double (&v)[8], int lane) {
+  // lanes 0-31 rows 0..3, lanes 32-63 rows 4..7
+  const double s0 = swap_add<32>(v[0], v[4]), s1 = swap_add<32>(v[1], v[5]);
+  const double s2 = swap_add<32>(v[2], v[6]), s3 = swap_add<32>(v[3], v[7]);
+  // 16-lane groups: t0 rows 0, 2, 4, 6; t1 rows 1, 3, 5, 7
+  const double t0 = swap_add<16>(s0, s2), t1 = swap_add<16>(s1, s3);
+  // 8-lane groups: lanes with bit 3 clear keep t0's row, set keep t1's
+  const bool b3 = (lane & 8) != 0;
+  const double keep = b3 ? t1 : t0, give = b3 ? t0 : t1;
+  double r = keep + wv_dpp<0x128>(give);  // row_ror 8: lane l ^ 8 within 16
+  r += wv_dpp<0x141>(r);                  // row_half_mirror: i <-> 7 - i
+  r += wv_dpp<0xB1>(r);                   // quad_perm [1, 0, 3, 2]
+  r += wv_dpp<0x4E>(r);                   // quad_perm [2, 3, 0, 1]
+  return r;
+}
+
+__device__ __forceinline__ double rdlane_f64(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
+  const __bf16 x = (__bf16)a, y = (__bf16)b;
+  return (unsigned)__builtin_bit_cast(unsigned short, x) |
+         ((unsigned)__builtin_bit_cast(unsigned short, y) << 16);
 }
 }  // namespace
 
-template <bool STD, int NT16>
-__global__ __launch_bounds__(512, 1) void wide_gram_all_bf16_kernel(const WideArgs a) {
-  constexpr int S = zall_groups(NT16);
-  constexpr int T = NT16 * (NT16 + 1) / 2;
-  constexpr int TG = (T + S - 1) / S;    // tiles per group
-  constexpr int TPW = (TG + 7) / 8;      // tiles per wave
+template <bool STD, int NT16, bool VEC2>
+__global__ __launch_bounds__(64 * FW, 1) void wide_fused_bf16_kernel(const WideArgs a) {
+  constexpr int S = fused_groups(NT16);
   constexpr int PP = 16 * NT16;
-  constexpr int ITEMS = PP * 4 / 512;    // (feature, 8-row group) items per thread
-  extern __shared__ __attribute__((aligned(16))) char zimg[];  // [2][PP][ZS]
+  constexpr int NF = PP / 64;     // columns per lane of each row
+  constexpr int HALF = NT16 / 2;  // tile-row pairs
+  constexpr int PPS = fused_pairs_per_slot(NT16);
+  constexpr int TPP = NT16 + 1;   // tiles per pair
+  constexpr int NT = 64 * FW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* zimg = smem;                            // [2][PP][FZ]
+  double* bl = (double*)(smem + 2 * PP * FZ);   // [PP] beta (x 1/scale) by column
+  double* sd = bl + PP;                         // [2][PP] 1/scale, center/scale (STD)
+  double* red = sd + 2 * PP;                    // [FW][PP] gradient of each wave
+  double* misc = red + FW * PP;                 // [0] eta offset, [8..] log-lik, [16..] sum r
 
   const int bid = blockIdx.x;
   const int xcd = bid & 7, j8 = bid >> 3;
   const int sg = j8 % S, cl = j8 / S;
-  const int chunk = cl * 8 + xcd;  // the S groups of a row group on one XCD
+  const int chunk = cl * 8 + xcd;  // the S workgroups of a row group on one XCD
   if (chunk >= a.n_gchunks) return;
-  const int part = a.gc_part[chunk];
-  if (a.phase[part] != a.want_phase) return;  // workgroup-uniform
+  const int part = __builtin_amdgcn_readfirstlane(a.gc_part[chunk]);
+  if (a.phase[part] != PHASE_F32) return;  // workgroup-uniform
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int p = a.p, ic = a.intercept;
+  const int p = a.p, P = a.P, ic = a.intercept;
   const int64_t row0 = a.gc_row0[chunk];
-  const int nrows = a.gc_rows[chunk];
+  const int nrows = __builtin_amdgcn_readfirstlane(a.gc_rows[chunk]);
   const int nb = (nrows + 31) / 32;
+  const double* th = a.theta + (int64_t)part * P;
 
-  // this wave's tiles (wave-uniform registers)
-  int tI[TPW], tJ[TPW];
-  bool tv[TPW];
-#pragma unroll
-  for (int i = 0; i < TPW; ++i) {
-    const int t = sg * TG + wid * TPW + i;
-    tv[i] = (wid * TPW + i < TG) && t < T;
-    int I = 0;
-    while ((I + 1) * (I + 2) / 2 <= t) ++I;
-    tI[i] = __builtin_amdgcn_readfirstlane(tv[i] ? I : 0);
-    tJ[i] = __builtin_amdgcn_readfirstlane(tv[i] ? t - I * (I + 1) / 2 : 0);
-  }
-
-  // staging items: feature f = (tid + 512 m) % PP, rows 8 g .. 8 g + 7
-  int colx[ITEMS], fz[ITEMS], gz[ITEMS];
-  bool inx[ITEMS], onex[ITEMS];
-  double cx[ITEMS], sx[ITEMS];
-#pragma unroll
-  for (int m = 0; m < ITEMS; ++m) {
-    const int idx = tid + 512 * m;
-    const int f = idx % PP, g = idx / PP;
-    fz[m] = f;
-    gz[m] = g;
-    const int jj = f - ic;
-    inx[m] = jj >= 0 && jj < p;
-    onex[m] = ic && f == 0;
-    colx[m] = inx[m] ? jj : 0;
-    cx[m] = 0.0;
-    sx[m] = 1.0;
+  // ---- setup: zero Z images (padding features stay 0), beta, eta offset ----
+  for (int o = tid * 16; o < 2 * PP * FZ; o += NT * 16) *(uint4*)(zimg + o) = make_uint4(0, 0, 0, 0);
+  for (int c = tid; c < PP; c += NT) {
+    double is = 1.0, cs = 0.0;
     if constexpr (STD) {
-      if (inx[m]) {
-        cx[m] = a.center[jj];
-        sx[m] = 1.0 / a.scale[jj];
+      if (c < p) {
+        is = 1.0 / a.scale[c];
+        cs = a.center[c] * is;
       }
     }
+    bl[c] = c < p ? th[c + ic] * is : 0.0;
+    sd[c] = is;
+    sd[PP + c] = cs;
   }
+  if (wid == 0) {  // eta offset: intercept - sum_c beta_c center_c / scale_c
+    double s = 0.0;
+    if constexpr (STD)
+      for (int c = lane; c < p; c += 64) s += th[c + ic] * (a.center[c] / a.scale[c]);
+    s = wave_allsum(s);
+    if (lane == 0) misc[0] = (ic ? th[0] : 0.0) - s;
+  }
+  __syncthreads();
+  const double eoff = bcast_first(misc[0]);
 
-  double xb[ITEMS][8];
-  auto load = [&](int b) {
+  auto colf = [&](int m) { return VEC2 ? 2 * lane + 128 * (m >> 1) + (m & 1) : lane + 64 * m; };
+  const int rl = lane >> 3;  // the row this lane's transcendental work is for
+
+  // per-lane byte offset of each column group in the wave's first row (out of
+  // range columns: an offset past any buffer -> reads 0); row u adds u p 8
+  // through the uniform soffset
+  constexpr int NV = VEC2 ? NF / 2 : NF;
+  int voff[NV];
 #pragma unroll
-    for (int m = 0; m < ITEMS; ++m)
+  for (int v = 0; v < NV; ++v) {
+    const int c = colf(VEC2 ? 2 * v : v);
+    voff[v] = c < p ? (8 * wid * p + c) * 8 : 0x7FFFFFF0;
+  }
+  double xv[8][NF];
+  double yv = 0.0;
+  auto issue = [&](int b) {
+    const int64_t rb = row0 + 32LL * b;
+    const int rows = min(32, nrows - 32 * b);
+    const __amdgpu_buffer_rsrc_t xr =
+        wv_rsrc((uintptr_t)(a.X + rb * p), (uintptr_t)rows * (uintptr_t)p * 8u);
+    const __amdgpu_buffer_rsrc_t yr = wv_rsrc((uintptr_t)(a.y + rb), (uintptr_t)rows * 8u);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        int r = 32 * b + 8 * gz[m] + e;
-        r = r < nrows ? r : nrows - 1;
-        xb[m][e] = a.X[(row0 + r) * (int64_t)p + colx[m]];
+    for (int u = 0; u < 8; ++u) {
+      const int so = u * p * 8;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        if constexpr (VEC2) {
+          const d2w d =
+              __builtin_bit_cast(d2w, __builtin_amdgcn_raw_buffer_load_b128(xr, voff[v], so, 0));
+          xv[u][2 * v] = d.x;
+          xv[u][2 * v + 1] = d.y;
+        } else {
+          xv[u][v] =
+              __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xr, voff[v], so, 0));
+        }
       }
-  };
-  auto stage = [&](int b) {
-    char* img = zimg + (b & 1) * (PP * ZS);
-    // sqrt(w) of the block's 32 rows: lane l (< 32) holds row l, broadcast by
-    // v_readlane (the row of an item is wave-uniform); rows past the chunk: 0
-    const int rl = 32 * b + (lane & 31);
-    const float swl = rl < nrows ? sqrtf((float)a.w[row0 + rl]) : 0.f;
-#pragma unroll
-    for (int m = 0; m < ITEMS; ++m) {
-      bf16x8w z;
-      const int g8 = __builtin_amdgcn_readfirstlane(8 * gz[m]);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float sw = __builtin_bit_cast(
-            float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, swl), g8 + e));
-        double v = inx[m] ? xb[m][e] : 0.0;
-        if constexpr (STD) v = (v - cx[m]) * sx[m];
-        if (onex[m]) v = 1.0;
-        float vf = (float)v;
-        asm volatile("" : "+v"(vf));  // keep f64 -> f32 -> bf16 (see irls_coop_impl.hpp)
-        z[e] = (__bf16)(vf * sw);
-      }
-      *(bf16x8w*)(img + fz[m] * ZS + 16 * gz[m]) = z;
     }
+    yv = __builtin_bit_cast(double,
+                            __builtin_amdgcn_raw_buffer_load_b64(yr, (8 * wid + rl) * 8, 0, 0));
   };
 
-  f4w acc[TPW];
+  double gacc[NF];
 #pragma unroll
-  for (int i = 0; i < TPW; ++i) acc[i] = f4w{0.f, 0.f, 0.f, 0.f};
+  for (int m = 0; m < NF; ++m) gacc[m] = 0.0;
+  // log-lik: sum of y eta - max(eta, 0) on the first lane of each row group,
+  // and the softplus term as a running product of t = 1 + exp(-|eta|) in
+  // [1, 2] kept as mantissa x 2^lexp (frexp each block: exact) -- one log per
+  // lane at the end instead of one per row, and no more rounding than a sum
+  // of per-row logs
+  double rsum = 0.0, llacc = 0.0, lprod = 1.0;
+  int lexp = 0;
+  f4w acc[PPS][TPP];
+#pragma unroll
+  for (int k = 0; k < PPS; ++k)
+#pragma unroll
+    for (int i = 0; i < TPP; ++i) acc[k][i] = f4w{0.f, 0.f, 0.f, 0.f};
+  const int slot = sg * FW + wid;
   const int fl = lane & 15, kg = lane >> 4;
 
-  if (nb > 0) load(0);
+  if (nb > 0) issue(0);
   for (int b = 0; b < nb; ++b) {
-    stage(b);
-    if (b + 1 < nb) load(b + 1);  // in flight during the barrier and the MFMAs
-    __syncthreads();              // image b complete; every wave is past block b-1
-    const char* img = zimg + (b & 1) * (PP * ZS);
+    // ---- row phase -----------------------------------------------------------
+    double e8[8];
 #pragma unroll
-    for (int i = 0; i < TPW; ++i) {
-      if (tv[i]) {  // wave-uniform
-        const bf16x8w av = *(const bf16x8w*)(img + (16 * tI[i] + fl) * ZS + 16 * kg);
-        const bf16x8w bv = *(const bf16x8w*)(img + (16 * tJ[i] + fl) * ZS + 16 * kg);
-        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[i], 0, 0, 0);
+    for (int u = 0; u < 8; ++u) {
+      double e0 = 0.0, e1 = 0.0;
+#pragma unroll
+      for (int m = 0; m < NF; ++m) {
+        const double bm = bl[colf(m)];
+        if (m & 1)
+          e1 = fma(xv[u][m], bm, e1);
+        else
+          e0 = fma(xv[u][m], bm, e0);
+      }
+      e8[u] = e0 + e1;
+    }
+    const double eu = reduce_scatter8(e8, lane) + eoff;
+    const bool vrow = 32 * b + 8 * wid + rl < nrows;
+    const double ea = exp(-fabs(eu));
+    const double inv = wv_rcp(1.0 + ea);
+    const double mu = eu >= 0.0 ? inv : ea * inv;
+    const double w = ea * inv * inv;  // mu (1 - mu), cancellation free
+    const double r = vrow ? yv - mu : 0.0;
+    if (sg == 0 && (lane & 7) == 0 && vrow) {
+      llacc += yv * eu - fmax(eu, 0.0);
+      lprod *= 1.0 + ea;
+    }
+    {
+      int e2;
+      lprod = frexp(lprod, &e2);
+      lexp += e2;
+    }
+    const float swl = vrow ? sqrtf((float)w) : 0.f;
+    float sw[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      sw[u] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, swl), 8 * u));
+    if (sg == 0) {  // workgroup-uniform: group 0 accumulates the gradient
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const double ru = rdlane_f64(r, 8 * u);
+        rsum += ru;
+#pragma unroll
+        for (int m = 0; m < NF; ++m) gacc[m] = fma(xv[u][m], ru, gacc[m]);
+      }
+    }
+    // Z image of the block: this wave's 8 rows of each of the lane's columns
+    char* zb = zimg + (b & 1) * (PP * FZ);
+#pragma unroll
+    for (int m = 0; m < NF; ++m) {
+      const int c = colf(m);
+      float zf[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        double v = xv[u][m];
+        if constexpr (STD) v = fma(v, sd[c], -sd[PP + c]);
+        float f = (float)v;
+        asm volatile("" : "+v"(f));  // keep f64 -> f32 -> bf16 (see irls_coop_impl.hpp)
+        zf[u] = f * sw[u];
+      }
+      // columns c >= p read as 0 and write 0 into padding features; only the
+      // last column can map past the image (c + ic = PP)
+      if (m < NF - 1 || c + ic < PP)
+        *(uint4*)(zb + (c + ic) * FZ + 16 * wid) =
+            make_uint4(pack_bf16x2(zf[0], zf[1]), pack_bf16x2(zf[2], zf[3]),
+                       pack_bf16x2(zf[4], zf[5]), pack_bf16x2(zf[6], zf[7]));
+    }
+    if (ic && lane == 0)  // intercept column: z = sqrt(w)
+      *(uint4*)(zb + 16 * wid) =
+          make_uint4(pack_bf16x2(sw[0], sw[1]), pack_bf16x2(sw[2], sw[3]),
+                     pack_bf16x2(sw[4], sw[5]), pack_bf16x2(sw[6], sw[7]));
+
+    if (b + 1 < nb) issue(b + 1);  // in flight across the barrier and the MFMAs
+    // this wave's Z writes done; every wave's image b complete and image b-1 consumed
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+
+    // ---- MFMA phase: per pair q, tile rows NT16 - 1 - q (J < nh) and q ------
+    const char* base = zimg + (b & 1) * (PP * FZ) + fl * FZ + 16 * kg;
+#pragma unroll
+    for (int k = 0; k < PPS; ++k) {
+      const int q = slot + FW * S * k;
+      if (q < HALF) {  // wave-uniform
+        const int nh = NT16 - q;  // tiles of the upper row (>= HALF + 1)
+        const bf16x8w ahi = *(const bf16x8w*)(base + 16 * (NT16 - 1 - q) * FZ);
+        const bf16x8w alo = *(const bf16x8w*)(base + 16 * q * FZ);
+        // groups of 2 tiles, operands of group g+1 read during the MFMAs of
+        // group g; the scheduling barriers keep the compiler from hoisting
+        // every operand read to the top
+        constexpr int GS = 2, NG = (TPP + GS - 1) / GS;
+        bf16x8w bq[2][GS];
+        auto rd = [&](int g, bf16x8w* dst) {
+#pragma unroll
+          for (int j = 0; j < GS; ++j) {
+            const int i = g * GS + j;
+            if (i < TPP) {
+              const int J = (i <= HALF || i < nh) ? i : i - nh;
+              dst[j] = *(const bf16x8w*)(base + 16 * J * FZ);
+            }
+          }
+        };
+        rd(0, bq[0]);
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+          if (g + 1 < NG) rd(g + 1, bq[(g + 1) & 1]);
+#pragma unroll
+          for (int j = 0; j < GS; ++j) {
+            const int i = g * GS + j;
+            if (i < TPP) {
+              const bool hi = i <= HALF || i < nh;
+              acc[k][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hi ? ahi : alo, bq[g & 1][j],
+                                                                  acc[k][i], 0, 0, 0);
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+    // keep the accumulators in AGPRs across the loop back edge (the first 64
+    // tiles: 256 AGPRs; at PP = 512 the last 2 tiles of a slot stay in VGPRs)
+#pragma unroll
+    for (int k = 0; k < PPS; ++k)
+#pragma unroll
+      for (int i = 0; i < TPP; ++i) {
+        if (k * TPP + i < 64)
+          asm volatile("" : "+a"(acc[k][i]));
+        else
+          asm volatile("" : "+v"(acc[k][i]));
+      }
+  }
+
+  // ---- epilogue: Gram tiles (C/D map of the f32 16x16 MFMAs: row = 4 kg + r,
+  // column = fl), 128 x 128-tile slab layout -----------------------------------
+  {
+    constexpr int NB = NT16 / 8;
+    constexpr int TB = NB * (NB + 1) / 2;
+#pragma unroll
+    for (int k = 0; k < PPS; ++k) {
+      const int q = slot + FW * S * k;
+      if (q >= HALF) continue;
+      const int nh = NT16 - q;
+#pragma unroll
+      for (int i = 0; i < TPP; ++i) {
+        const bool hi = i <= HALF || i < nh;
+        const int I = hi ? NT16 - 1 - q : q;
+        const int J = hi ? i : i - nh;
+        const int I8 = I >> 3, J8 = J >> 3;
+        double* G = a.slab_G + ((int64_t)chunk * TB + I8 * (I8 + 1) / 2 + J8) * (GT * GT);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          G[(16 * (I & 7) + 4 * kg + r) * GT + 16 * (J & 7) + fl] = (double)acc[k][i][r];
       }
     }
   }
-
-  // C/D map of the f32 16x16 MFMAs: row = 4 (l >> 4) + r, column = l & 15
-  constexpr int NB = NT16 / 8;
-  constexpr int TB = NB * (NB + 1) / 2;
+  if (sg != 0) return;  // workgroup-uniform: group 0 publishes the gradient
+  // ---- gradient / log-lik partials: fixed-order sum over the waves ---------
 #pragma unroll
-  for (int i = 0; i < TPW; ++i) {
-    if (!tv[i]) continue;
-    const int I = tI[i], J = tJ[i];
-    const int I8 = I >> 3, J8 = J >> 3;
-    const int t128 = I8 * (I8 + 1) / 2 + J8;
-    double* G = a.slab_G + ((int64_t)chunk * TB + t128) * (GT * GT);
+  for (int m = 0; m < NF; ++m) red[wid * PP + colf(m)] = gacc[m];
+  if ((lane & 7) == 0) llacc -= log(lprod) + lexp * 0.6931471805599453094;
+  llacc = wave_allsum(llacc);
+  if (lane == 0) {
+    misc[8 + wid] = llacc;
+    misc[16 + wid] = rsum;
+  }
+  __syncthreads();
+  double rs = 0.0;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int il = 16 * (I & 7) + 4 * kg + r;
-      const int jl = 16 * (J & 7) + fl;
-      G[il * GT + jl] = (double)acc[i][r];
+  for (int v = 0; v < FW; ++v) rs += misc[16 + v];
+  for (int f = tid; f < PP; f += NT) {
+    const int c = f - ic;
+    double g = 0.0;
+    if (ic && f == 0) {
+      g = rs;
+    } else if (c < p) {
+      double s = 0.0;
+#pragma unroll
+      for (int v = 0; v < FW; ++v) s += red[v * PP + c];
+      g = STD ? fma(sd[c], s, -sd[PP + c] * rs) : s;
     }
+    a.slab_gz[(int64_t)chunk * PP + f] = g;
+  }
+  if (tid == 0) {
+    double ll = 0.0;
+#pragma unroll
+    for (int v = 0; v < FW; ++v) ll += misc[8 + v];
+    a.slab_llz[chunk] = ll;
   }
 }
 
 template <bool STD, int NT16>
-static hipError_t launch_gram_all_t(const WideArgs& a, hipStream_t s) {
-  auto kern = wide_gram_all_bf16_kernel<STD, NT16>;
-  const int lds = 2 * 16 * NT16 * ZS;
+static hipError_t launch_fused_t(const WideArgs& a, hipStream_t s) {
+  const bool vec2 = (a.p % 2 == 0) && ((uintptr_t)a.X % 16 == 0);
+  const void* kern = vec2 ? (const void*)wide_fused_bf16_kernel<STD, NT16, true>
+                          : (const void*)wide_fused_bf16_kernel<STD, NT16, false>;
+  const int lds = fused_lds_bytes(NT16);
   {
-    hipError_t e = ensure_max_lds((const void*)kern, lds);
+    hipError_t e = ensure_max_lds(kern, lds);
     if (e != hipSuccess) return e;
   }
-  const int grid = ((a.n_gchunks + 7) / 8) * 8 * zall_groups(NT16);
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, s, a);
+  const int grid = ((a.n_gchunks + 7) / 8) * 8 * fused_groups(NT16);
+  if (vec2)
+    hipLaunchKernelGGL((wide_fused_bf16_kernel<STD, NT16, true>), dim3(grid), dim3(64 * FW), lds, s,
+                       a);
+  else
+    hipLaunchKernelGGL((wide_fused_bf16_kernel<STD, NT16, false>), dim3(grid), dim3(64 * FW), lds,
+                       s, a);
   return hipGetLastError();
 }
 
-// workgroups per row group of the all-tiles bf16 Gram pass (plan sizing)
-int wide_gram_all_groups(int NB) { return zall_groups(8 * NB); }
-
-hipError_t launch_wide_gram_all(const WideArgs& a, bool standardize, hipStream_t s) {
+hipError_t launch_wide_fused(const WideArgs& a, bool standardize, hipStream_t s) {
   if (a.n_gchunks <= 0) return hipSuccess;
   switch (a.NB) {
-    case 2: return standardize ? launch_gram_all_t<true, 16>(a, s) : launch_gram_all_t<false, 16>(a, s);
-    case 3: return standardize ? launch_gram_all_t<true, 24>(a, s) : launch_gram_all_t<false, 24>(a, s);
-    case 4: return standardize ? launch_gram_all_t<true, 32>(a, s) : launch_gram_all_t<false, 32>(a, s);
+    case 2: return standardize ? launch_fused_t<true, 16>(a, s) : launch_fused_t<false, 16>(a, s);
+    case 3: return standardize ? launch_fused_t<true, 24>(a, s) : launch_fused_t<false, 24>(a, s);
+    case 4: return standardize ? launch_fused_t<true, 32>(a, s) : launch_fused_t<false, 32>(a, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -669,7 +785,8 @@ __global__ __launch_bounds__(256) void wide_assemble_kernel(const WideArgs a, co
 // per-partition Newton update (one 1024-thread workgroup per partition)
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, const WideArgs wa,
-                                                           const int32_t* rcb, double* Hfull) {
+                                                           const int32_t* rcb, const int32_t* gcb,
+                                                           double* Hfull) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int k = blockIdx.x;
   if (a.status[k] != STATUS_RUNNING) return;
@@ -684,16 +801,20 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
   int* flag = (int*)(red + 48);
   double* H = Hfull + (int64_t)k * PP * PP;
 
-  // 1. gradient and log-likelihood of the pass (row-chunk order)
-  const int cb = rcb[k], ce = rcb[k + 1];
+  // 1. gradient and log-likelihood of the pass, in chunk order: the fused
+  // pass's row groups (PHASE_F32) or the row pass's chunks (PHASE_F64)
+  const bool fz = a.phase[k] == PHASE_F32;
+  const int cb = fz ? gcb[k] : rcb[k], ce = fz ? gcb[k + 1] : rcb[k + 1];
+  const double* sg = fz ? wa.slab_gz : wa.slab_g;
+  const double* sll = fz ? wa.slab_llz : wa.slab_ll;
   for (int f = tid; f < PP; f += 1024) {
     double s = 0.0;
-    for (int c = cb; c < ce; ++c) s += wa.slab_g[(int64_t)c * PP + f];
+    for (int c = cb; c < ce; ++c) s += sg[(int64_t)c * PP + f];
     g[f] = f < P ? s : 0.0;
   }
   if (wid == 0) {
     double s = 0.0;
-    for (int c = cb + lane; c < ce; c += 64) s += wa.slab_ll[c];
+    for (int c = cb + lane; c < ce; c += 64) s += sll[c];
     s = wave_sum64(s);
     if (lane == 0) red[40] = s;
   }
@@ -1017,18 +1138,11 @@ hipError_t launch_wide_row(const WideArgs& a, bool standardize, int family, int 
   }
 }
 
-hipError_t launch_wide_gram(const WideArgs& a, bool standardize, bool f64, hipStream_t s) {
+// exact (fp64) Gram pass of the PHASE_F64 partitions
+hipError_t launch_wide_gram(const WideArgs& a, bool standardize, hipStream_t s) {
   if (a.n_gchunks <= 0) return hipSuccess;
   const int TB = a.NB * (a.NB + 1) / 2;
   const int grid = ((a.n_gchunks + 7) / 8) * 8 * TB;
-  if (!f64) {
-    if (!getenv("DLSA_WIDE_GRAM_TILED")) return launch_wide_gram_all(a, standardize, s);
-    if (standardize)
-      hipLaunchKernelGGL(wide_gram_bf16_kernel<true>, dim3(grid), dim3(512), 0, s, a);
-    else
-      hipLaunchKernelGGL(wide_gram_bf16_kernel<false>, dim3(grid), dim3(512), 0, s, a);
-    return hipGetLastError();
-  }
   if (standardize)
     hipLaunchKernelGGL(wide_gram_kernel<true>, dim3(grid), dim3(512), 0, s, a);
   else
@@ -1044,13 +1158,13 @@ hipError_t launch_wide_assemble(const WideArgs& a, const int32_t* gcb, double* H
 }
 
 hipError_t launch_wide_newton(const SolveArgs& sa, const WideArgs& wa, const int32_t* rcb,
-                              double* Hfull, int K, hipStream_t s) {
+                              const int32_t* gcb, double* Hfull, int K, hipStream_t s) {
   {
     hipError_t e = ensure_max_lds((const void*)wide_newton_kernel, 160 * 1024);
     if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL(wide_newton_kernel, dim3(K), dim3(1024), wide_newton_lds_bytes(wa.NB), s,
-                     sa, wa, rcb, Hfull);
+                     sa, wa, rcb, gcb, Hfull);
   return hipGetLastError();
 }
 

@@ -347,6 +347,32 @@ def test_wide_shapes_vs_oracle(torch_cuda, M, p, fi, std):
     assert np.array_equal(S_, np.transpose(S_, (0, 2, 1)))
 
 
+@pytest.mark.parametrize("p,fi,std", [(300, True, False), (301, False, True), (450, True, True)])
+def test_wide_fused_pass_gradient_fixed_point(torch_cuda, M, p, fi, std):
+    """The fused bf16 pass's fp64 gradient / log-lik: run the approximate
+    phase to a step of 1e-12 (switch_tol), so it stops at the zero of ITS
+    gradient; if that gradient is the true X^T (y - mu), the exact phase then
+    accepts the point in ONE fp64 pass and the fit matches the oracle.
+    Even / odd p (16-byte / 8-byte row loads), intercept, standardisation."""
+    n = 14 * p + 333
+    X, y = O.simulate_counter(n, p, seed=p + 11)
+    center = scale = None
+    if std:
+        X = X * 1.5 - 0.2
+        center, scale = X.mean(0), X.std(0)
+    off = np.array([0, n], dtype=np.int64)
+    fit = M.logistic_model_batched(X, y, off, fit_intercept=fi, center=center, scale=scale,
+                                   switch_tol=1e-12, rows_per_chunk=1500)
+    assert fit.stats["passes_fp32"] >= 3
+    assert fit.stats["passes_fp64"] == 1
+    th, S, St, ll, it = O.logistic_fit_partitions(X, y, off, fit_intercept=fi, center=center,
+                                                  scale=scale)
+    assert int(fit.status[0]) == 0
+    assert _rel(fit.theta.cpu(), th) < REL
+    assert _rel(fit.sig_inv.cpu(), S) < REL
+    assert _rel(fit.loglik.cpu(), ll) < 1e-10
+
+
 def test_wide_auto_chunking_and_determinism(torch_cuda, M):
     """Default (automatic) row-chunk / row-group plan, and bit-identical
     results across two runs (fixed-order reductions everywhere)."""
