@@ -329,14 +329,13 @@ __global__ __launch_bounds__(512, 1) void wide_gram_kernel(const WideArgs a) {
 //   2. w, r, log-lik: ONE fp64 exp / reciprocal sequence for the 8 rows,
 //      broadcast by readlane; the softplus sum is a running product
 //      (frexp-normalised), one log per lane at the end;
-//   3. gradient FMAs (group 0 only) and the Z image of the block in LDS:
-//      feature-major [PP][32 rows] bf16, 80-byte feature stride (the 16 lanes
-//      of an MFMA operand read hit 16 distinct bank groups), one
-//      ds_write_b128 per (lane, column) = the wave's 8 rows of that feature;
-//   4. the loads of block b+1 are issued into the same registers, one LDS
-//      barrier (no vmcnt drain), and the MFMA phase: v_mfma_f32_16x16x32_bf16
-//      with operand lane (i, kg) = feature i, rows 8 kg .. 8 kg + 7 (one
-//      ds_read_b128) -- the loads stay in flight behind it.
+//   3. per half of 4 rows: gradient FMAs (group 0 only), the half's Z plane
+//      (see zplane_bytes), and the loads of the same half of block b+1 into
+//      the freed registers -- in flight across the other half, the barrier
+//      and the MFMA phase;
+//   4. one LDS barrier (no vmcnt drain) and the MFMA phase:
+//      v_mfma_f32_16x16x32_bf16, operand lane (i, kg) = feature i, rows
+//      8 kg .. 8 kg + 7.
 // Wave slot s = 4 sg + w owns the tile-row pairs q = s + 4 S k: rows q and
 // NT16 - 1 - q, NT16 + 1 tiles per pair (2 pairs = 66 tiles at PP = 512).
 // Double-buffered Z images: one barrier per block.  Output: the
@@ -345,20 +344,28 @@ __global__ __launch_bounds__(512, 1) void wide_gram_kernel(const WideArgs a) {
 // deterministic.
 // ---------------------------------------------------------------------------
 typedef __bf16 bf16x8w __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4w __attribute__((ext_vector_type(4)));
 typedef float f4w __attribute__((ext_vector_type(4)));
 typedef double d2w __attribute__((ext_vector_type(2)));
 
 namespace {
-constexpr int FZ = 80;  // bytes per feature of a Z image: 32 rows of bf16 + 16 B pad
 constexpr int FW = 4;   // waves per workgroup of the fused pass
+// Z image of a 32-row block: 8 planes (wave w, half h = rows 8w + 4h .. +3),
+// each [PP features][4 rows] bf16 (8 B per feature) + 64 B pad.  A half's
+// store (one ds_write_b64 per lane and column, features 2 apart across the
+// lanes) is 2-way conflicted; an MFMA operand (feature i, rows 8 kg .. +7) is
+// two ds_read_b64 from planes 2 kg and 2 kg + 1, conflict-free: the plane
+// pad moves kg = 1 (lanes 16-31) onto the other 32 banks of lanes 0-15.
+__host__ __device__ constexpr int zplane_bytes(int NT16) { return 16 * NT16 * 8 + 64; }
+__host__ __device__ constexpr int zimg_bytes(int NT16) { return 8 * zplane_bytes(NT16); }
 __host__ __device__ constexpr int fused_groups(int NT16) { return NT16 > 16 ? 2 : 1; }
 __host__ __device__ constexpr int fused_pairs_per_slot(int NT16) {
   return (NT16 / 2 + FW * fused_groups(NT16) - 1) / (FW * fused_groups(NT16));
 }
-// [2][PP][FZ] Z images, [PP] scaled beta, [2][PP] 1/scale and center/scale,
+// [2] Z images, [PP] scaled beta, [2][PP] 1/scale and center/scale,
 // [FW][PP] gradient reduction, [32] misc
 __host__ __device__ constexpr int fused_lds_bytes(int NT16) {
-  return 2 * 16 * NT16 * FZ + (3 + FW) * 16 * NT16 * 8 + 256;
+  return 2 * zimg_bytes(NT16) + (3 + FW) * 16 * NT16 * 8 + 256;
 }
 
 // Sum over the 64 lanes; every lane ends with the bitwise-identical total
@@ -392,6 +399,21 @@ __device__ __forceinline__ double swap_add(double a, double b) {
   }
 }
 
+// 4 row partials per lane -> lane l holds the total of row l >> 4 (every lane
+// of the 16-lane group bitwise-identical)
+__device__ __forceinline__ double reduce_scatter4(const double (&v)[4], int lane) {
+  (void)lane;
+  // lanes 0-31 rows 0, 1; lanes 32-63 rows 2, 3
+  const double s0 = swap_add<32>(v[0], v[2]), s1 = swap_add<32>(v[1], v[3]);
+  // 16-lane groups: rows 0, 1, 2, 3
+  double r = swap_add<16>(s0, s1);
+  r += wv_dpp<0x141>(r);  // row_half_mirror: i <-> 7 - i
+  r += wv_dpp<0xB1>(r);   // quad_perm [1, 0, 3, 2]
+  r += wv_dpp<0x4E>(r);   // quad_perm [2, 3, 0, 1]
+  r += wv_dpp<0x140>(r);  // row_mirror: i <-> 15 - i
+  return r;
+}
+
 // 8 row partials per lane -> lane l holds the total of row l >> 3 (every lane
 // of the 8-lane group bitwise-identical)
 __device__ __forceinline__ double reduce_scatter8(const double (&v)[8], int lane) {
@@ -416,10 +438,10 @@ __device__ __forceinline__ double rdlane_f64(double v, int l) {
   return __hiloint2double(hi, lo);
 }
 
-__device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
-  const __bf16 x = (__bf16)a, y = (__bf16)b;
-  return (unsigned)__builtin_bit_cast(unsigned short, x) |
-         ((unsigned)__builtin_bit_cast(unsigned short, y) << 16);
+typedef float f2w __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2w __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {  // v_cvt_pk_bf16_f32
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(f2w{a, b}, bf16x2w));
 }
 }  // namespace
 
@@ -433,8 +455,9 @@ __global__ __launch_bounds__(64 * FW, 1) void wide_fused_bf16_kernel(const WideA
   constexpr int TPP = NT16 + 1;   // tiles per pair
   constexpr int NT = 64 * FW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* zimg = smem;                            // [2][PP][FZ]
-  double* bl = (double*)(smem + 2 * PP * FZ);   // [PP] beta (x 1/scale) by column
+  constexpr int ZPL = zplane_bytes(NT16), ZIMG = zimg_bytes(NT16);
+  char* zimg = smem;                            // [2] Z images
+  double* bl = (double*)(smem + 2 * ZIMG);      // [PP] beta (x 1/scale) by column
   double* sd = bl + PP;                         // [2][PP] 1/scale, center/scale (STD)
   double* red = sd + 2 * PP;                    // [FW][PP] gradient of each wave
   double* misc = red + FW * PP;                 // [0] eta offset, [8..] log-lik, [16..] sum r
@@ -455,7 +478,7 @@ __global__ __launch_bounds__(64 * FW, 1) void wide_fused_bf16_kernel(const WideA
   const double* th = a.theta + (int64_t)part * P;
 
   // ---- setup: zero Z images (padding features stay 0), beta, eta offset ----
-  for (int o = tid * 16; o < 2 * PP * FZ; o += NT * 16) *(uint4*)(zimg + o) = make_uint4(0, 0, 0, 0);
+  for (int o = tid * 16; o < 2 * ZIMG; o += NT * 16) *(uint4*)(zimg + o) = make_uint4(0, 0, 0, 0);
   for (int c = tid; c < PP; c += NT) {
     double is = 1.0, cs = 0.0;
     if constexpr (STD) {
@@ -479,7 +502,7 @@ __global__ __launch_bounds__(64 * FW, 1) void wide_fused_bf16_kernel(const WideA
   const double eoff = bcast_first(misc[0]);
 
   auto colf = [&](int m) { return VEC2 ? 2 * lane + 128 * (m >> 1) + (m & 1) : lane + 64 * m; };
-  const int rl = lane >> 3;  // the row this lane's transcendental work is for
+  const int rl = lane >> 3;  // the row of the wave this lane's transcendental work is for
 
   // per-lane byte offset of each column group in the wave's first row (out of
   // range columns: an offset past any buffer -> reads 0); row u adds u p 8
@@ -493,14 +516,19 @@ __global__ __launch_bounds__(64 * FW, 1) void wide_fused_bf16_kernel(const WideA
   }
   double xv[8][NF];
   double yv = 0.0;
-  auto issue = [&](int b) {
+  // rows 4 h .. 4 h + 3 of this wave in block b (with h = 0: y of row rl).
+  // Block nb (one past the last) is issued too, with an empty buffer range
+  // (all loads return 0, no memory access): every loop iteration then has
+  // the same loads in flight, so the compiler's vmcnt bookkeeping never
+  // merges an "issued" and a "not issued" path into a full drain.
+  auto issue = [&](int b, int h) {
     const int64_t rb = row0 + 32LL * b;
-    const int rows = min(32, nrows - 32 * b);
+    const int rows = max(0, min(32, nrows - 32 * b));
     const __amdgpu_buffer_rsrc_t xr =
         wv_rsrc((uintptr_t)(a.X + rb * p), (uintptr_t)rows * (uintptr_t)p * 8u);
     const __amdgpu_buffer_rsrc_t yr = wv_rsrc((uintptr_t)(a.y + rb), (uintptr_t)rows * 8u);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 4 * h; u < 4 * h + 4; ++u) {
       const int so = u * p * 8;
 #pragma unroll
       for (int v = 0; v < NV; ++v) {
@@ -515,8 +543,9 @@ __global__ __launch_bounds__(64 * FW, 1) void wide_fused_bf16_kernel(const WideA
         }
       }
     }
-    yv = __builtin_bit_cast(double,
-                            __builtin_amdgcn_raw_buffer_load_b64(yr, (8 * wid + rl) * 8, 0, 0));
+    if (h == 0)
+      yv = __builtin_bit_cast(double,
+                              __builtin_amdgcn_raw_buffer_load_b64(yr, (8 * wid + rl) * 8, 0, 0));
   };
 
   double gacc[NF];
@@ -537,9 +566,15 @@ __global__ __launch_bounds__(64 * FW, 1) void wide_fused_bf16_kernel(const WideA
   const int slot = sg * FW + wid;
   const int fl = lane & 15, kg = lane >> 4;
 
-  if (nb > 0) issue(0);
+  if (nb > 0) {
+    issue(0, 0);
+    issue(0, 1);
+  }
   for (int b = 0; b < nb; ++b) {
-    // ---- row phase -----------------------------------------------------------
+    // ---- row phase: eta, w, r, log-lik of the wave's 8 rows (one
+    // transcendental sequence), then per half of 4 rows the gradient, the Z
+    // entries and the loads of that half of block b+1: those stay in flight
+    // across the other half, the barrier and the MFMA phase ----------------
     double e8[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -554,7 +589,7 @@ __global__ __launch_bounds__(64 * FW, 1) void wide_fused_bf16_kernel(const WideA
       }
       e8[u] = e0 + e1;
     }
-    const double eu = reduce_scatter8(e8, lane) + eoff;
+    const double eu = reduce_scatter8(e8, lane) + eoff;  // row rl of the wave
     const bool vrow = 32 * b + 8 * wid + rl < nrows;
     const double ea = exp(-fabs(eu));
     const double inv = wv_rcp(1.0 + ea);
@@ -571,86 +606,85 @@ __global__ __launch_bounds__(64 * FW, 1) void wide_fused_bf16_kernel(const WideA
       lexp += e2;
     }
     const float swl = vrow ? sqrtf((float)w) : 0.f;
-    float sw[8];
+    char* zb = zimg + (b & 1) * ZIMG;
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
-      sw[u] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, swl), 8 * u));
-    if (sg == 0) {  // workgroup-uniform: group 0 accumulates the gradient
+    for (int h = 0; h < 2; ++h) {
+      float sw[4];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const double ru = rdlane_f64(r, 8 * u);
-        rsum += ru;
+      for (int u = 0; u < 4; ++u)
+        sw[u] = __builtin_bit_cast(
+            float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, swl), 8 * (4 * h + u)));
+      if (sg == 0) {  // workgroup-uniform: group 0 accumulates the gradient
 #pragma unroll
-        for (int m = 0; m < NF; ++m) gacc[m] = fma(xv[u][m], ru, gacc[m]);
+        for (int u = 0; u < 4; ++u) {
+          const double ru = rdlane_f64(r, 8 * (4 * h + u));
+          rsum += ru;
+#pragma unroll
+          for (int m = 0; m < NF; ++m) gacc[m] = fma(xv[4 * h + u][m], ru, gacc[m]);
+        }
       }
-    }
-    // Z image of the block: this wave's 8 rows of each of the lane's columns
-    char* zb = zimg + (b & 1) * (PP * FZ);
+      // Z entries: plane (wid, h), this half's 4 rows of each of the lane's columns
+      char* zp = zb + (2 * wid + h) * ZPL;
 #pragma unroll
-    for (int m = 0; m < NF; ++m) {
-      const int c = colf(m);
-      float zf[8];
+      for (int m = 0; m < NF; ++m) {
+        const int c = colf(m);
+        float zf[4];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        double v = xv[u][m];
-        if constexpr (STD) v = fma(v, sd[c], -sd[PP + c]);
-        float f = (float)v;
-        asm volatile("" : "+v"(f));  // keep f64 -> f32 -> bf16 (see irls_coop_impl.hpp)
-        zf[u] = f * sw[u];
+        for (int u = 0; u < 4; ++u) {
+          double v = xv[4 * h + u][m];
+          if constexpr (STD) v = fma(v, sd[c], -sd[PP + c]);
+          float f = (float)v;
+          asm volatile("" : "+v"(f));  // keep f64 -> f32 -> bf16 (see irls_coop_impl.hpp)
+          zf[u] = f * sw[u];
+        }
+        // columns c >= p read as 0 and write 0 into padding features; only the
+        // last column can map past the plane (c + ic = PP)
+        if (m < NF - 1 || c + ic < PP)
+          *(uint2*)(zp + (c + ic) * 8) = make_uint2(pack_bf16x2(zf[0], zf[1]), pack_bf16x2(zf[2], zf[3]));
       }
-      // columns c >= p read as 0 and write 0 into padding features; only the
-      // last column can map past the image (c + ic = PP)
-      if (m < NF - 1 || c + ic < PP)
-        *(uint4*)(zb + (c + ic) * FZ + 16 * wid) =
-            make_uint4(pack_bf16x2(zf[0], zf[1]), pack_bf16x2(zf[2], zf[3]),
-                       pack_bf16x2(zf[4], zf[5]), pack_bf16x2(zf[6], zf[7]));
+      if (ic && lane == 0)  // intercept column: z = sqrt(w)
+        *(uint2*)zp = make_uint2(pack_bf16x2(sw[0], sw[1]), pack_bf16x2(sw[2], sw[3]));
+      issue(b + 1, h);
     }
-    if (ic && lane == 0)  // intercept column: z = sqrt(w)
-      *(uint4*)(zb + 16 * wid) =
-          make_uint4(pack_bf16x2(sw[0], sw[1]), pack_bf16x2(sw[2], sw[3]),
-                     pack_bf16x2(sw[4], sw[5]), pack_bf16x2(sw[6], sw[7]));
-
-    if (b + 1 < nb) issue(b + 1);  // in flight across the barrier and the MFMAs
     // this wave's Z writes done; every wave's image b complete and image b-1 consumed
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
     // ---- MFMA phase: per pair q, tile rows NT16 - 1 - q (J < nh) and q ------
-    const char* base = zimg + (b & 1) * (PP * FZ) + fl * FZ + 16 * kg;
+    // operand (feature 16 J + fl, rows 8 kg .. 8 kg + 7): planes 2 kg, 2 kg + 1
+    const char* base = zimg + (b & 1) * ZIMG + 2 * kg * ZPL + fl * 8;
+    auto op = [&](int J) {
+      const bf16x4w lo = *(const bf16x4w*)(base + 16 * J * 8);
+      const bf16x4w hi = *(const bf16x4w*)(base + ZPL + 16 * J * 8);
+      return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    };
+    // Tile i of pair q: the upper row NT16 - 1 - q holds i < nh = NT16 - q
+    // (J = i), the lower row q the rest, stored from the end (J = NT16 - i).
+    // Over the slots that share pair index k, q spans [qlo, qhi], so tiles
+    // i < NT16 - qhi are upper-row and i >= NT16 - qlo lower-row for every
+    // slot -- compile-time operands; only the 7 tiles in between pick their
+    // row at run time (uniform LDS offsets, no register selects).
+    constexpr int D = 2;  // B operands read D tiles ahead of their MFMA
 #pragma unroll
     for (int k = 0; k < PPS; ++k) {
       const int q = slot + FW * S * k;
       if (q < HALF) {  // wave-uniform
-        const int nh = NT16 - q;  // tiles of the upper row (>= HALF + 1)
-        const bf16x8w ahi = *(const bf16x8w*)(base + 16 * (NT16 - 1 - q) * FZ);
-        const bf16x8w alo = *(const bf16x8w*)(base + 16 * q * FZ);
-        // groups of 2 tiles, operands of group g+1 read during the MFMAs of
-        // group g; the scheduling barriers keep the compiler from hoisting
-        // every operand read to the top
-        constexpr int GS = 2, NG = (TPP + GS - 1) / GS;
-        bf16x8w bq[2][GS];
-        auto rd = [&](int g, bf16x8w* dst) {
-#pragma unroll
-          for (int j = 0; j < GS; ++j) {
-            const int i = g * GS + j;
-            if (i < TPP) {
-              const int J = (i <= HALF || i < nh) ? i : i - nh;
-              dst[j] = *(const bf16x8w*)(base + 16 * J * FZ);
-            }
-          }
+        const int nh = NT16 - q;
+        const int qlo = FW * S * k, qhi = min(HALF - 1, FW * S * k + FW * S - 1);
+        const int st_hi = NT16 - qhi, st_lo = NT16 - qlo;  // compile-time after unrolling
+        const bf16x8w ahi = op(NT16 - 1 - q), alo = op(q);
+        auto jof = [&](int i) { return (i < st_hi || (i < st_lo && i < nh)) ? i : NT16 - i; };
+        bf16x8w bq[D + 1], aq[D + 1];
+        auto rd = [&](int i) {
+          bq[i % (D + 1)] = op(jof(i));
+          if (i >= st_hi && i < st_lo) aq[i % (D + 1)] = op(i < nh ? NT16 - 1 - q : q);
         };
-        rd(0, bq[0]);
 #pragma unroll
-        for (int g = 0; g < NG; ++g) {
-          if (g + 1 < NG) rd(g + 1, bq[(g + 1) & 1]);
+        for (int i = 0; i < D; ++i) rd(i);
 #pragma unroll
-          for (int j = 0; j < GS; ++j) {
-            const int i = g * GS + j;
-            if (i < TPP) {
-              const bool hi = i <= HALF || i < nh;
-              acc[k][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hi ? ahi : alo, bq[g & 1][j],
-                                                                  acc[k][i], 0, 0, 0);
-            }
-          }
+        for (int i = 0; i < TPP; ++i) {
+          if (i + D < TPP) rd(i + D);
+          const bf16x8w av = i < st_hi ? ahi : (i >= st_lo ? alo : aq[i % (D + 1)]);
+          acc[k][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bq[i % (D + 1)], acc[k][i], 0, 0, 0);
           __builtin_amdgcn_sched_barrier(0);
         }
       }
@@ -680,9 +714,9 @@ __global__ __launch_bounds__(64 * FW, 1) void wide_fused_bf16_kernel(const WideA
       const int nh = NT16 - q;
 #pragma unroll
       for (int i = 0; i < TPP; ++i) {
-        const bool hi = i <= HALF || i < nh;
+        const bool hi = i < nh;
         const int I = hi ? NT16 - 1 - q : q;
-        const int J = hi ? i : i - nh;
+        const int J = hi ? i : NT16 - i;
         const int I8 = I >> 3, J8 = J >> 3;
         double* G = a.slab_G + ((int64_t)chunk * TB + I8 * (I8 + 1) / 2 + J8) * (GT * GT);
 #pragma unroll
