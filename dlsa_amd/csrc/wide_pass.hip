@@ -348,6 +348,10 @@ typedef __bf16 bf16x4w __attribute__((ext_vector_type(4)));
 typedef float f4w __attribute__((ext_vector_type(4)));
 typedef double d2w __attribute__((ext_vector_type(2)));
 
+#ifndef DLSA_FUSED_ABLATE
+#define DLSA_FUSED_ABLATE 0
+#endif
+
 namespace {
 constexpr int FW = 4;   // waves per workgroup of the fused pass
 // Z image of a 32-row block: 8 planes (wave w, half h = rows 8w + 4h .. +3),
@@ -522,7 +526,11 @@ __global__ __launch_bounds__(64 * FW, 1) void wide_fused_bf16_kernel(const WideA
   // the same loads in flight, so the compiler's vmcnt bookkeeping never
   // merges an "issued" and a "not issued" path into a full drain.
   auto issue = [&](int b, int h) {
+#if DLSA_FUSED_ABLATE == 1  // profiling only: every block re-reads block 0 (L2-resident)
+    const int64_t rb = row0 + 32LL * min(b, nb > 0 ? 0 : b);
+#else
     const int64_t rb = row0 + 32LL * b;
+#endif
     const int rows = max(0, min(32, nrows - 32 * b));
     const __amdgpu_buffer_rsrc_t xr =
         wv_rsrc((uintptr_t)(a.X + rb * p), (uintptr_t)rows * (uintptr_t)p * 8u);

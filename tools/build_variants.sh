@@ -18,6 +18,7 @@ for v in "$@"; do
     cat16) D=DLSA_CAT_ABLATE=16 ;;
     solveprof) D=DLSA_SOLVE_PROFILE=1 ;;
     cat31) D=DLSA_CAT_ABLATE=31 ;;
+    fab1) D=DLSA_FUSED_ABLATE=1 ;;
     nt) D=DLSA_X_DMA_AUX=2 ;;
     sc1) D=DLSA_X_DMA_AUX=1 ;;
     *) echo "unknown variant $v"; exit 1 ;;
