@@ -210,6 +210,8 @@ static void make_wide_plans(const int64_t* offsets, int K, int p, int intercept,
                                                                 int64_t(1) << 24));
   if (rows_per_chunk > 0) rpc_row = rpc_gram = rows_per_chunk;
   if (const char* e = getenv("DLSA_WIDE_GRAM_ROWS")) rpc_gram = std::max(64, atoi(e));
+  // the Gram kernels address a row group's X with 32-bit buffer offsets
+  rpc_gram = (int)std::min<int64_t>(rpc_gram, (int64_t(1) << 30) / (8LL * std::max(p, 1)));
   make_plan(offsets, K, p, intercept, rpc_row, wp.rows, frac, min_rows);
   make_plan(offsets, K, p, intercept, rpc_gram, wp.gram, frac, min_rows);
 }

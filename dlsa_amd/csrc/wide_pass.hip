@@ -167,14 +167,20 @@ __global__ __launch_bounds__(256) void wide_row_kernel(const WideArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// gram pass: 512 threads = 8 waves per 128x128 output tile (I, J), I >= J.
-// Wave (qi = wid >> 1, qj = wid & 1) owns rows 32 qi .. +31 and columns
-// 64 qj .. +63 of the tile: 2 x 4 accumulators of v_mfma_f64_16x16x4_f64.
-// K dimension = rows: per k-step of 4 rows lane l reads row (l >> 4) of the
-// step at feature (l & 15) of each 16-wide sub-tile (A = w x, B = x).
+// exact Gram pass: 256 threads = 4 waves per 128x128 output tile (I, J),
+// I >= J; wave (qi = w >> 1, qj = w & 1) owns the 64 x 64 quadrant rows
+// 64 qi .., columns 64 qj .. (the strictly-upper quadrant of a diagonal tile
+// is skipped): 4 x 4 accumulators of v_mfma_f64_16x16x4_f64 (128 AGPRs), 16
+// MFMAs per k-step of 4 rows against 8 operand loads + w -- fp64 VALU work
+// and fp64 MFMAs do not overlap on a SIMD, so the VALU per MFMA is what the
+// wave tile has to minimise.  Operands come straight from X by raw buffer
+// loads: lane l reads row (l >> 4) of the k-step at feature (l & 15) of each
+// 16-wide sub-tile, per-lane offsets fixed, the k-step advancing the uniform
+// soffset (no address VALU); rows past the row group and columns >= p read 0
+// through the buffer range check.  Four k-steps of operands in flight.
 // ---------------------------------------------------------------------------
 template <bool STD>
-__global__ __launch_bounds__(512, 1) void wide_gram_kernel(const WideArgs a) {
+__global__ __launch_bounds__(256, 2) void wide_gram_kernel(const WideArgs a) {
   const int NB = a.NB;
   const int TB = NB * (NB + 1) / 2;
   const int bid = blockIdx.x;
@@ -189,118 +195,113 @@ __global__ __launch_bounds__(512, 1) void wide_gram_kernel(const WideArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int qi = wid >> 1, qj = wid & 1;
-  if (I == J && qj == 1 && qi < 2) return;  // strictly-upper quadrant of a diagonal tile
+  if (I == J && qi == 0 && qj == 1) return;  // strictly-upper quadrant of a diagonal tile
   const int p = a.p, ic = a.intercept;
   const int64_t row0 = a.gc_row0[chunk];
-  const int nrows = a.gc_rows[chunk];
+  const int nrows = __builtin_amdgcn_readfirstlane(a.gc_rows[chunk]);
   const int fl = lane & 15, kq = lane >> 4;
 
-  // per-lane feature columns of the 2 A sub-tiles and the 4 B sub-tiles
-  int colA[2], colB[4];
-  bool inA[2], inB[4], oneA[2], oneB[4];
-  double cA[2], sA[2], cB[4], sB[4];
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const int f = GT * I + 32 * qi + 16 * s + fl, jj = f - ic;
-    inA[s] = jj >= 0 && jj < p;
-    oneA[s] = ic && f == 0;
-    colA[s] = inA[s] ? jj : 0;
-    cA[s] = 0.0;
-    sA[s] = 1.0;
-    if constexpr (STD) {
-      if (inA[s]) {
-        cA[s] = a.center[jj];
-        sA[s] = 1.0 / a.scale[jj];
-      }
-    }
-  }
+  // per-lane operand offsets (row kq of a k-step), 0x80000000 = column >= p
+  int offA[4], offB[4];
+  bool oneA = false, oneB = false;
+  double cA[4], sA[4], cB[4], sB[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    const int f = GT * J + 64 * qj + 16 * s + fl, jj = f - ic;
-    inB[s] = jj >= 0 && jj < p;
-    oneB[s] = ic && f == 0;
-    colB[s] = inB[s] ? jj : 0;
-    cB[s] = 0.0;
-    sB[s] = 1.0;
+    const int fa = GT * I + 64 * qi + 16 * s + fl, ja = fa - ic;
+    const int fb = GT * J + 64 * qj + 16 * s + fl, jb = fb - ic;
+    offA[s] = (ja >= 0 && ja < p) ? (kq * p + ja) * 8 : (int)0x80000000;
+    offB[s] = (jb >= 0 && jb < p) ? (kq * p + jb) * 8 : (int)0x80000000;
+    if (s == 0) {
+      oneA = ic && fa == 0;
+      oneB = ic && fb == 0;
+    }
+    cA[s] = cB[s] = 0.0;
+    sA[s] = sB[s] = 1.0;
     if constexpr (STD) {
-      if (inB[s]) {
-        cB[s] = a.center[jj];
-        sB[s] = 1.0 / a.scale[jj];
+      if (ja >= 0 && ja < p) {
+        sA[s] = 1.0 / a.scale[ja];
+        cA[s] = a.center[ja] * sA[s];
+      }
+      if (jb >= 0 && jb < p) {
+        sB[s] = 1.0 / a.scale[jb];
+        cB[s] = a.center[jb] * sB[s];
       }
     }
   }
+  const __amdgpu_buffer_rsrc_t xr =
+      wv_rsrc((uintptr_t)(a.X + row0 * p), (uintptr_t)nrows * (uintptr_t)p * 8u);
+  const __amdgpu_buffer_rsrc_t wr = wv_rsrc((uintptr_t)(a.w + row0), (uintptr_t)nrows * 8u);
 
-  d4w acc[2][4];
+  d4w acc[4][4];
 #pragma unroll
-  for (int s = 0; s < 2; ++s)
+  for (int s = 0; s < 4; ++s)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) acc[s][b] = d4w{0, 0, 0, 0};
+    for (int u = 0; u < 4; ++u) acc[s][u] = d4w{0, 0, 0, 0};
 
-  constexpr int U = 4;  // k-steps per prefetch group (16 rows)
   struct Frag {
-    double xa[U][2], xb[U][4], w[U];
+    double xa[4], xb[4], w;
   };
-  auto load = [&](int step0, Frag& F) {
+  auto load = [&](int step, Frag& F) {
+    const int so = step * 4 * p * 8;  // k-step rows 4 step .. 4 step + 3
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int r = 4 * (step0 + u) + kq;
-      const bool valid = r < nrows;
-      const int rc = valid ? r : nrows - 1;  // in-partition address, weight 0
-      const double* xr = a.X + (row0 + rc) * (int64_t)p;
-      F.w[u] = valid ? a.w[row0 + rc] : 0.0;
-#pragma unroll
-      for (int s = 0; s < 2; ++s) F.xa[u][s] = xr[colA[s]];
-#pragma unroll
-      for (int s = 0; s < 4; ++s) F.xb[u][s] = xr[colB[s]];
+    for (int s = 0; s < 4; ++s) {
+      F.xa[s] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xr, offA[s], so, 0));
+      F.xb[s] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xr, offB[s], so, 0));
     }
+    F.w = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(wr, kq * 8, step * 32, 0));
   };
   auto compute = [&](const Frag& F) {
+    double av[4], bv[4];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      double av[2], bv[4];
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        double v = inA[s] ? F.xa[u][s] : 0.0;
-        if constexpr (STD) v = (v - cA[s]) * sA[s];
-        if (oneA[s]) v = 1.0;
-        av[s] = v * F.w[u];
+    for (int s = 0; s < 4; ++s) {
+      double x = F.xa[s], z = F.xb[s];
+      if constexpr (STD) {
+        x = fma(x, sA[s], -cA[s]);
+        z = fma(z, sB[s], -cB[s]);
       }
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        double v = inB[s] ? F.xb[u][s] : 0.0;
-        if constexpr (STD) v = (v - cB[s]) * sB[s];
-        if (oneB[s]) v = 1.0;
-        bv[s] = v;
+      if (s == 0) {
+        if (oneA) x = 1.0;
+        if (oneB) z = 1.0;
       }
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-          acc[s][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[b], acc[s][b], 0, 0, 0);
+      av[s] = x * F.w;  // rows past the group: w = 0
+      bv[s] = z;
     }
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        acc[s][u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[u], acc[s][u], 0, 0, 0);
   };
   const int nsteps = (nrows + 3) / 4;
+  constexpr int DEPTH = 4;  // k-steps of operands in flight
   if (nsteps > 0) {
-    Frag cur, nxt;
-    load(0, cur);
-    for (int s0 = 0; s0 < nsteps; s0 += U) {
-      if (s0 + U < nsteps) load(s0 + U, nxt);
-      compute(cur);  // steps past nsteps have w = 0: no contribution
-      cur = nxt;
+    Frag f[DEPTH];
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) load(d, f[d]);  // past the end: range-checked zeros
+    for (int s0 = 0; s0 < nsteps; s0 += DEPTH) {  // a ragged last group adds zeros
+#pragma unroll
+      for (int d = 0; d < DEPTH; ++d) {
+        compute(f[d]);
+        load(s0 + DEPTH + d, f[d]);
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) asm volatile("" : "+a"(acc[s][u]));
     }
   }
 
   // C/D map of the f64 16x16x4 MFMA: row = (l >> 4) + 4 r, column = l & 15
   double* G = a.slab_G + ((int64_t)chunk * TB + t) * (GT * GT);
 #pragma unroll
-  for (int s = 0; s < 2; ++s)
+  for (int s = 0; s < 4; ++s)
 #pragma unroll
-    for (int b = 0; b < 4; ++b)
+    for (int u = 0; u < 4; ++u)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int i = 32 * qi + 16 * s + kq + 4 * r;
-        const int jc = 64 * qj + 16 * b + fl;
-        G[i * GT + jc] = acc[s][b][r];
+        const int i = 64 * qi + 16 * s + kq + 4 * r;
+        const int jc = 64 * qj + 16 * u + fl;
+        G[i * GT + jc] = acc[s][u][r];
       }
 }
 
@@ -1186,9 +1187,9 @@ hipError_t launch_wide_gram(const WideArgs& a, bool standardize, hipStream_t s) 
   const int TB = a.NB * (a.NB + 1) / 2;
   const int grid = ((a.n_gchunks + 7) / 8) * 8 * TB;
   if (standardize)
-    hipLaunchKernelGGL(wide_gram_kernel<true>, dim3(grid), dim3(512), 0, s, a);
+    hipLaunchKernelGGL(wide_gram_kernel<true>, dim3(grid), dim3(256), 0, s, a);
   else
-    hipLaunchKernelGGL(wide_gram_kernel<false>, dim3(grid), dim3(512), 0, s, a);
+    hipLaunchKernelGGL(wide_gram_kernel<false>, dim3(grid), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
