@@ -637,6 +637,7 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
       DLSA_HIP_TRY(timed(&g_stats.ms_wide_assemble,
                          [&] { return launch_wide_assemble(wa, d_gcb, d_H, K, stream); }));
       DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
+      sa.last_iter = it + 1 == it_end ? 1 : 0;
       DLSA_HIP_TRY(timed(&g_stats.ms_solve,
                          [&] { return launch_wide_newton(sa, wa, d_rcb, d_gcb, d_H, K, stream); }));
       DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, stream));

@@ -78,6 +78,7 @@ struct SolveArgs {
   double tol;
   double switch_tol;
   double level_tol;   // warm-start level: stop when max|step| <= level_tol (1+max|theta|)
+  int32_t last_iter;  // wide path: the last iteration of the budget (publish Sig_inv)
 };
 
 // Arguments of the log-likelihood evaluation pass.

@@ -898,12 +898,17 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
     }
     return;
   }
-  // 3. publish the information matrix at the evaluation point (models.py:130)
+  // 3. publish the information matrix at the evaluation point (models.py:130):
+  // exact-phase passes, and the last iteration of the budget (a partition that
+  // stops in the approximate phase keeps its last Hessian); the copy of P^2
+  // values by one workgroup is skipped on the approximate iterations in between
   if (!a.subsample) {
-    double* S = a.sig_inv + (int64_t)k * P * P;
-    for (int e = tid; e < P * P; e += 1024) {
-      const int i = e / P, j = e - i * P;
-      S[e] = H[(int64_t)i * PP + j];
+    if (phase == PHASE_F64 || a.last_iter) {
+      double* S = a.sig_inv + (int64_t)k * P * P;
+      for (int e = tid; e < P * P; e += 1024) {
+        const int i = e / P, j = e - i * P;
+        S[e] = H[(int64_t)i * PP + j];
+      }
     }
     if (tid == 0) a.loglik[k] = ll;
   }
