@@ -241,9 +241,11 @@ def main():
     torch.cuda.synchronize()
 
     stats_acc = []
+    stage_ms = {"fit": 0.0, "reduce_allreduce": 0.0, "wlse_lars_dbic": 0.0}
 
     def step(record):
         nonlocal ws
+        t_a = time.perf_counter()
         if family == "ols":
             fit = ols_model_batched(X, y, offsets, record_timing=record, device=dev)
         elif codes_layout:
@@ -256,14 +258,21 @@ def main():
                                          record_timing=record, workspace=ws, device=dev)
             if ws.numel() < fit.stats["workspace_bytes"]:
                 ws = torch.empty((fit.stats["workspace_bytes"],), dtype=torch.uint8, device=dev)
+        t_b = time.perf_counter()  # the fit returns after its stream synchronisation
         buf = reduce_partitions_device(fit, n_rows=True)
         combine(buf)  # the one collective: RCCL all-reduce over xGMI (no-op at N = 1)
         b = buf.cpu().numpy()
+        t_c = time.perf_counter()
         S, v, st, Ksum = split_reduced(b[:-1], fit.P)
         est = wlse(S, v)
         lars = lars_lsa(S, est, fit_intercept, int(round(b[-1])), type="lasso")
         ib = int(np.argmin(lars["BIC"]))
         support = np.nonzero(lars["beta"][ib])[0]
+        if record:  # per-rank wall-clock budget of a step
+            t_d = time.perf_counter()
+            stage_ms["fit"] += (t_b - t_a) * 1e3
+            stage_ms["reduce_allreduce"] += (t_c - t_b) * 1e3
+            stage_ms["wlse_lars_dbic"] += (t_d - t_c) * 1e3
         return fit, est, support, int(round(Ksum)), int(round(b[-1]))
 
     for _ in range(args.warmup):
@@ -321,10 +330,11 @@ def main():
         n32, n64 = tot("passes_fp32"), tot("passes_fp64")
         rows32, rows64 = tot("rows_fp32"), tot("rows_fp64")
         ms32, ms64, ms_row = tot("ms_pass_fp32"), tot("ms_pass_fp64"), tot("ms_wide_row")
-        kern["wide_row_kernel"] = {"ms_per_step": ms_row / args.steps,
-                                   "GBps": (rows32 + rows64) * row_bytes / (ms_row * 1e-3) / 1e9}
+        if n64:  # the exact passes' row pass (eta, w, gradient; the fused pass does its own)
+            kern["wide_row_kernel"] = {"ms_per_step": ms_row / args.steps,
+                                       "GBps": rows64 * row_bytes / (ms_row * 1e-3) / 1e9}
         if n32:
-            kern["wide_gram_bf16_kernel"] = {
+            kern["wide_fused_bf16_kernel"] = {
                 "launches_per_step": n32 / args.steps, "avg_launch_ms": ms32 / n32,
                 "GBps": rows32 * row_bytes / (ms32 * 1e-3) / 1e9,
                 "alg_TFps": rows32 * p * (p + 1) / (ms32 * 1e-3) / 1e12,
@@ -346,8 +356,9 @@ def main():
                     "mfma_issued_TFps": rows64 * gram_flops_row / (ms64 * 1e-3) / 1e12}
             pmc_key = "wide_gram_kernel<fp64>"
         else:
-            roof = hbm_roof("wide_gram_bf16_kernel (approximate X^T W X)", ms32, n32, rows32)
-            pmc_key = "wide_gram_bf16_kernel"
+            roof = hbm_roof("wide_fused_bf16_kernel (one X stream per iteration: gradient + "
+                            "approximate X^T W X)", ms32, n32, rows32)
+            pmc_key = "wide_fused_bf16"
     else:
         NT = (P + 15) // 16
         mfma_flops_per_row = NT * (NT + 1) // 2 * 16 * 16 * 2  # lower-triangle 16x16 tiles
@@ -433,6 +444,7 @@ def main():
                                   "P^2+2P+2 fp64)"},
         "roofline": roof,
         "kernels": kern,
+        "stages_ms_per_step": {k: v / args.steps for k, v in stage_ms.items()},
         "newton": {"iterations": last["iterations"], "passes_fp32": last["passes_fp32"],
                    "passes_fp64": last["passes_fp64"], "n_chunks": last["n_chunks"],
                    "status": fit.status_counts()},

@@ -1079,7 +1079,8 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
   const int64_t off_counts = align_up(L.total, 256);
   const int64_t off_bad = align_up(off_counts + 4LL * std::max(pl.n_chunks, 1) * std::max(D, 1), 256);
   const int64_t off_badp = align_up(off_bad + 4LL * std::max(pl.n_chunks, 1), 256);
-  const int64_t total = align_up(off_badp + 4LL * K, 256);
+  const int64_t off_colmax = align_up(off_badp + 4LL * K, 256);
+  const int64_t total = align_up(off_colmax + 8LL * kCatQMax * std::max(pl.n_chunks, 1), 256);
   g_stats.n_chunks = pl.n_chunks;
 
   char* ws = (char*)opt.workspace;
@@ -1109,6 +1110,7 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
   int32_t* d_counts = (int32_t*)at(off_counts);
   int32_t* d_bad = (int32_t*)at(off_bad);
   int32_t* d_badp = (int32_t*)at(off_badp);
+  double* d_colmax = (double*)at(off_colmax);
 
   auto upload = [&](const Plan& qn) -> hipError_t {
     hipError_t e = hipSuccess;
@@ -1148,16 +1150,45 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
   ca.want_phase = PHASE_F64;
 
   // level presence over all rows: partitions missing a level -> zero frame;
-  // invalid codes fail the call
+  // invalid codes fail the call.  The same pass takes max |x_i| per column for
+  // the fixed-point grids of the histograms (cat_pass.hip).
   std::vector<int32_t> h_phase(K, 0), h_badp(K, 0);
+  std::vector<double> h_colmax((size_t)kCatQMax * std::max(pl.n_chunks, 1), 0.0);
   DLSA_HIP_TRY(upload(pl));
+  DLSA_HIP_TRY(launch_cat_presence(ca, pl.n_chunks, d_counts, d_bad, d_colmax, stream));
+  if (pl.n_chunks > 0)
+    DLSA_HIP_TRY(hipMemcpyAsync(h_colmax.data(), d_colmax, 8LL * kCatQMax * pl.n_chunks,
+                                hipMemcpyDeviceToHost, stream));
   if (D > 0) {
-    DLSA_HIP_TRY(launch_cat_presence(ca, pl.n_chunks, d_counts, d_bad, stream));
     DLSA_HIP_TRY(launch_cat_mark(ca, d_pcb, d_counts, d_bad, K, d_phase, status, d_badp, stream));
     DLSA_HIP_TRY(hipMemcpyAsync(h_badp.data(), d_badp, 4LL * K, hipMemcpyDeviceToHost, stream));
   }
   DLSA_HIP_TRY(hipMemcpyAsync(h_phase.data(), d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
   DLSA_HIP_TRY(hipStreamSynchronize(stream));
+  {
+    // fixed-point grids: 2^E with |term| * 2^E * (rows of a chunk) <= 2^61
+    int64_t rmax = 1;
+    for (const Plan& qn : plans)
+      for (int c = 0; c < qn.n_chunks; ++c) rmax = std::max<int64_t>(rmax, qn.chunk_rows[c]);
+    auto grid = [&](double bound) {  // bound: max |term|
+      if (!(bound > 0) || !std::isfinite(bound)) bound = 1.0;
+      const int e = (int)std::floor(61.0 - std::log2(bound * (double)rmax));
+      return std::ldexp(1.0, std::max(-900, std::min(900, e)));
+    };
+    ca.hscale[0] = grid(0.25);  // w = mu (1 - mu) <= 1/4; pair cells
+    ca.hscale[1] = grid(1.0);   // |y - mu| <= 1
+    std::vector<double> hc(q, 0.0), hs(q, 1.0);
+    if (center && q > 0) {  // the kernel sums w (x - c) / s
+      DLSA_HIP_TRY(hipMemcpy(hc.data(), center, 8LL * q, hipMemcpyDeviceToHost));
+      DLSA_HIP_TRY(hipMemcpy(hs.data(), scale, 8LL * q, hipMemcpyDeviceToHost));
+    }
+    for (int j = 0; j < q; ++j) {
+      double m = 0.0;
+      for (int c = 0; c < pl.n_chunks; ++c) m = std::max(m, h_colmax[(size_t)c * kCatQMax + j]);
+      if (center) m = (m + std::fabs(hc[j])) / std::fabs(hs[j]);
+      ca.hscale[2 + j] = grid(0.25 * m);
+    }
+  }
   for (int k = 0; k < K; ++k)
     if (h_badp[k]) {
       set_error("partition " + std::to_string(k) + ": " + std::to_string(h_badp[k]) +

@@ -14,13 +14,18 @@
 //   dummy (f,l) x dummy (g,m)    sum_{code_f = l, code_g = m} w   2-D histogram
 //   gradient dummy (f,l)         sum_{code_f = l} (y - mu)
 //
-// All sums are fp64 (ds_add_f64): the Hessian is exact, so every pass is an
-// fp64 Newton pass and its H is Sig_inv.  Low-cardinality factors and pairs
-// keep several histogram replicas (lane & (R-1)) so the lanes of a wave that
-// share a frequent level do not serialise on one LDS address.  The order of
-// the fp64 additions inside a chunk follows the hardware's atomic order
-// (last-bit run-to-run differences; the chunk partials are then summed in a
-// fixed order).
+// The histogram bins are 64-bit FIXED-POINT integers (ds_add_u64): each term
+// is rounded once to a power-of-two grid chosen per column from the data's
+// range (scale 2^E with 0.25 max|x| 2^E x rows-per-chunk <= 2^61, so no bin
+// can overflow; for config 3 the grid step is ~1e-14 of the column's range),
+// then integer addition is exact and order-free -- the result is bit-identical
+// run to run whatever order the hardware applies the atomics in, and within
+// ~1e-13 relative of an fp64 sum.  The dense blocks (numeric x numeric,
+// gradient, log-lik) stay fp64 in registers with fixed-order reductions.  So
+// every pass is an exact Newton pass (its H is Sig_inv) and the whole fit is
+// deterministic.  Low-cardinality factors and pairs keep several histogram
+// replicas (lane & (R-1)) so the lanes of a wave that share a frequent level
+// do not serialise on one LDS address.
 //
 // Parameter order: [intercept] [q numeric] [factor 0: levels 1..L_0-1] ...
 // -- the reference's column order (sorted numeric names, then each factor's
@@ -43,8 +48,13 @@
 
 namespace dlsa {
 
-__device__ __forceinline__ void lds_add(double* p, double v) {
-  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+// fixed-point term: v * scale rounded to an integer (two's complement add)
+__device__ __forceinline__ void lds_add(unsigned long long* p, double v, double scale) {
+  const unsigned long long t = (unsigned long long)__double2ll_rn(v * scale);
+  __hip_atomic_fetch_add(p, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ long long hist_at(const unsigned long long* h, int i) {
+  return (long long)h[i];
 }
 
 // pair index of factors f < g among F
@@ -65,7 +75,7 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int q = a.q, F = a.F, P = a.P, ic = a.intercept;
   const int Qn = ic + q, Qw = q + 1;
-  double* hist = sm;                       // a.hist_doubles
+  unsigned long long* hist = (unsigned long long*)sm;  // a.hist_doubles int64 bins
   double* th = sm + a.hist_doubles;        // kCatPMax: theta of this partition
   double* stdv = th + kCatPMax;            // 2 x kCatQMax: center, 1 / scale
   double* red = stdv + 2 * kCatQMax;       // NW x NR, then NR final sums
@@ -91,7 +101,7 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
     t_proff[i] = a.pr_off[i];
     t_prrep[i] = a.pr_rep[i] - 1;
   }
-  for (int i = tid; i < a.hist_doubles; i += NTHR) hist[i] = 0.0;
+  for (int i = tid; i < a.hist_doubles; i += NTHR) hist[i] = 0ull;
   for (int i = tid; i < kCatPMax; i += NTHR) th[i] = i < P ? a.theta[(int64_t)part * P + i] : 0.0;
   if (STD && tid < kCatQMax) {
     stdv[tid] = tid < q ? a.center[tid] : 0.0;
@@ -159,19 +169,19 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
       for (int j = 0; j <= i; ++j) hacc[i * (i + 1) / 2 + j] = fma(wxi, xv[j], hacc[i * (i + 1) / 2 + j]);
     }
 
-    // one-hot blocks: histograms in LDS
+    // one-hot blocks: fixed-point histograms in LDS
 #pragma unroll
     for (int f = 0; f < FM; ++f) {
       if (f < F && cv[f] > 0) {
         const int slot = (lane & t_ndrep[f]) * t_nlev[f] + cv[f] - 1;
-        double* h = hist + t_ndoff[f] + slot * Qw;
+        unsigned long long* h = hist + t_ndoff[f] + slot * Qw;
         if constexpr (!(DLSA_CAT_ABLATE & 1)) {
-          lds_add(h, w);
+          lds_add(h, w, a.hscale[0]);
 #pragma unroll
           for (int i = 0; i < QN; ++i)  // numeric columns (register index compile-time)
-            if (i >= ic && i < Qn) lds_add(h + 1 + (i - ic), w * xv[i]);
+            if (i >= ic && i < Qn) lds_add(h + 1 + (i - ic), w * xv[i], a.hscale[2 + i - ic]);
         }
-        if constexpr (!(DLSA_CAT_ABLATE & 4)) lds_add(hist + t_goff[f] + slot, res);
+        if constexpr (!(DLSA_CAT_ABLATE & 4)) lds_add(hist + t_goff[f] + slot, res, a.hscale[1]);
       }
     }
 #pragma unroll
@@ -181,7 +191,8 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
         if (!(DLSA_CAT_ABLATE & 2) && g < F && cv[f] > 0 && cv[g] > 0) {
           const int pi = cat_pair(f, g, F);
           const int rep = lane & t_prrep[pi];
-          lds_add(hist + t_proff[pi] + (rep * t_nlev[f] + cv[f] - 1) * t_nlev[g] + cv[g] - 1, w);
+          lds_add(hist + t_proff[pi] + (rep * t_nlev[f] + cv[f] - 1) * t_nlev[g] + cv[g] - 1, w,
+                  a.hscale[0]);
         }
       }
   }
@@ -225,11 +236,12 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
     lev = gi - a.doff[f];
     return f;
   };
+  // exact integer sums over the replicas, one rounding back to fp64
   auto nd_sum = [&](int f, int lev, int col) {
     const int nl = a.nlev[f], R = a.nd_rep[f];
-    double s = 0.0;
-    for (int rp = 0; rp < R; ++rp) s += hist[a.nd_off[f] + (rp * nl + lev) * Qw + col];
-    return s;
+    long long s = 0;
+    for (int rp = 0; rp < R; ++rp) s += hist_at(hist, a.nd_off[f] + (rp * nl + lev) * Qw + col);
+    return (double)s / (col == 0 ? a.hscale[0] : a.hscale[1 + col]);
   };
 
   // ---- epilogue: the partial slab in the dense pass's tile format ---------
@@ -259,8 +271,9 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
           } else {  // fj < fi
             const int pi = cat_pair(fj, fi, F);
             const int nli = a.nlev[fi], nlj = a.nlev[fj], R = a.pr_rep[pi];
-            for (int rp = 0; rp < R; ++rp)
-              v += hist[a.pr_off[pi] + (rp * nlj + lj) * nli + li];
+            long long s = 0;
+            for (int rp = 0; rp < R; ++rp) s += hist_at(hist, a.pr_off[pi] + (rp * nlj + lj) * nli + li);
+            v = (double)s / a.hscale[0];
           }
         }
       }
@@ -276,7 +289,9 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
       int l;
       const int f = factor_of(e, l);
       const int nl = a.nlev[f], R = a.nd_rep[f];
-      for (int rp = 0; rp < R; ++rp) v += hist[a.g_off[f] + rp * nl + l];
+      long long s = 0;
+      for (int rp = 0; rp < R; ++rp) s += hist_at(hist, a.g_off[f] + rp * nl + l);
+      v = (double)s / a.hscale[1];
     }
     a.slab_g[(int64_t)chunk * PP + e] = v;
   }
@@ -284,10 +299,12 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
 }
 
 // Level presence per chunk: counts[chunk, d] = rows of the chunk whose code
-// selects dummy column d; bad[chunk] = codes outside 0..L_f-1.
+// selects dummy column d; bad[chunk] = codes outside 0..L_f-1; colmax[chunk, i]
+// = max |x_i| over the chunk (raw numeric columns: the fixed-point grids).
 __global__ __launch_bounds__(256) void cat_presence_kernel(const CatArgs a, int32_t* counts,
-                                                           int32_t* bad) {
+                                                           int32_t* bad, double* colmax) {
   __shared__ int32_t cnt[kCatPMax + 1];
+  __shared__ double cmax[4][kCatQMax];
   const int chunk = blockIdx.x, tid = threadIdx.x;
   const int D = a.P - a.intercept - a.q;
   const int F = a.F;
@@ -296,6 +313,9 @@ __global__ __launch_bounds__(256) void cat_presence_kernel(const CatArgs a, int3
   const int64_t row0 = a.chunk_row0[chunk];
   const int nrows = a.chunk_rows[chunk];
   const int doff0 = a.intercept + a.q;
+  double mx[kCatQMax];
+#pragma unroll
+  for (int i = 0; i < kCatQMax; ++i) mx[i] = 0.0;
   for (int r = tid; r < nrows; r += 256) {
     const uint8_t* cr = a.codes + (row0 + r) * F;
     for (int f = 0; f < F; ++f) {
@@ -305,10 +325,24 @@ __global__ __launch_bounds__(256) void cat_presence_kernel(const CatArgs a, int3
       else if (c > 0)
         atomicAdd(&cnt[a.doff[f] - doff0 + c - 1], 1);
     }
+    const double* xr = a.Xn + (row0 + r) * a.q;
+#pragma unroll
+    for (int i = 0; i < kCatQMax; ++i)
+      if (i < a.q) mx[i] = fmax(mx[i], fabs(xr[i]));  // NaN-ignoring: a NaN row fails the fit later
+  }
+  // max is order-free: wave butterfly, then the 4 waves
+#pragma unroll
+  for (int i = 0; i < kCatQMax; ++i) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) mx[i] = fmax(mx[i], __shfl_xor(mx[i], o));
+    if ((tid & 63) == 0) cmax[tid >> 6][i] = mx[i];
   }
   __syncthreads();
   for (int d = tid; d < D; d += 256) counts[(int64_t)chunk * D + d] = cnt[d];
   if (tid == 0) bad[chunk] = cnt[kCatPMax];
+  if (tid < a.q)
+    colmax[(int64_t)chunk * kCatQMax + tid] =
+        fmax(fmax(cmax[0][tid], cmax[1][tid]), fmax(cmax[2][tid], cmax[3][tid]));
 }
 
 // Per partition: a selected dummy level with no rows -> the reference's
@@ -395,9 +429,10 @@ hipError_t launch_cat_pass(const CatArgs& a, bool standardize, int n_chunks, hip
 }
 
 hipError_t launch_cat_presence(const CatArgs& a, int n_chunks, int32_t* counts, int32_t* bad,
-                               hipStream_t s) {
+                               double* colmax, hipStream_t s) {
   if (n_chunks <= 0) return hipSuccess;
-  hipLaunchKernelGGL(cat_presence_kernel, dim3(n_chunks), dim3(256), 0, s, a, counts, bad);
+  hipLaunchKernelGGL(cat_presence_kernel, dim3(n_chunks), dim3(256), 0, s, a, counts, bad,
+                     colmax);
   return hipGetLastError();
 }
 

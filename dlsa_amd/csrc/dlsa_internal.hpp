@@ -155,6 +155,9 @@ struct CatArgs {
   int32_t g_off[kCatMaxFactors];   // LDS: [rep][nlev] gradient
   int32_t pr_off[kCatMaxPairs];    // LDS: pair (f < g) [rep][nlev_f][nlev_g]
   int32_t pr_rep[kCatMaxPairs];
+  // fixed-point scales of the int64 histograms (power-of-two: [0] w and the
+  // pair cells, [1] the gradient residuals, [2 + i] w x_i of numeric column i)
+  double hscale[kCatQMax + 2];
 };
 
 // Row repartitioning (partition_rows.hip): stable counting sort by partition id.
@@ -175,6 +178,7 @@ hipError_t launch_cat_pass(const CatArgs& a, bool standardize, int n_chunks, hip
 size_t cat_lds_bytes(const CatArgs& a);  // dynamic LDS of the pass
 constexpr int kCatStaticLds = 4 * (5 * kCatMaxFactors + 2 * kCatMaxPairs);  // its tables
 hipError_t launch_cat_presence(const CatArgs& a, int n_chunks, int32_t* counts, int32_t* bad,
+                               double* colmax,
                                hipStream_t s);
 hipError_t launch_cat_mark(const CatArgs& a, const int32_t* pcb, const int32_t* counts,
                            const int32_t* bad, int K, int32_t* phase, int32_t* status,

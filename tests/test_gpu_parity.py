@@ -564,6 +564,31 @@ def test_categorical_config3_geometry_vs_oracle_and_dense(torch_cuda, M):
     assert _rel(fit.sig_inv.cpu()[keep], dense.sig_inv.cpu()[keep]) < REL
 
 
+def test_categorical_bit_identical_runs_and_column_ranges(torch_cuda, M):
+    """The one-hot histograms are fixed-point int64 sums (order-free), so two
+    runs are bit-identical; numeric columns of very different magnitudes
+    (x 1e3, x 1e-3, an offset column) get their own grids and still match the
+    oracle to the parity tolerance."""
+    torch = torch_cuda
+    Xn, codes, y, levels = M.simulate_categorical(3 * 30000, seed=11, device="cuda")
+    Xn = Xn.clone()
+    Xn[:, 0] *= 1e3
+    Xn[:, 1] *= 1e-3
+    Xn[:, 2] += 50.0
+    off = np.array([0, 30000, 60000, 90000], dtype=np.int64)
+    f1 = M.logistic_model_batched_categorical(Xn, codes, y, off, levels, fit_intercept=True)
+    f2 = M.logistic_model_batched_categorical(Xn, codes, y, off, levels, fit_intercept=True)
+    assert torch.equal(f1.theta, f2.theta) and torch.equal(f1.sig_inv, f2.sig_inv)
+    assert torch.equal(f1.loglik, f2.loglik)
+    assert (f1.status.cpu().numpy() == 0).all(), f1.status
+    X = O.expand_codes(Xn.cpu().numpy(), codes.cpu().numpy(), levels)
+    yh = y.cpu().numpy()
+    for k in (0, 2):
+        o = O.logistic_fit(X[off[k]:off[k + 1]], yh[off[k]:off[k + 1]], fit_intercept=True)
+        assert _rel(f1.theta[k].cpu(), o["coef"]) < REL
+        assert _rel(f1.sig_inv[k].cpu(), o["Sig_inv"]) < REL
+
+
 def test_categorical_invalid_code_fails_loudly(torch_cuda, M):
     from dlsa_amd._hip import DlsaHipError
 
