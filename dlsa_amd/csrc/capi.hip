@@ -931,7 +931,8 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
 // serialise the lanes of a wave on one address (nd: <= 128 slots per factor,
 // pairs: <= 512 cells), shrunk until the workgroup fits 160 KB.
 static bool cat_layout(CatArgs& a, const int32_t* levels) {
-  const int Qw = a.q + 1;
+  const int Qw = (a.q + 1) | 1;
+  a.nd_stride = Qw;
   int nd_cap = 128, pr_cap = 512;
   for (int attempt = 0; attempt < 12; ++attempt) {
     int64_t o = 0;

@@ -174,7 +174,7 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
     for (int f = 0; f < FM; ++f) {
       if (f < F && cv[f] > 0) {
         const int slot = (lane & t_ndrep[f]) * t_nlev[f] + cv[f] - 1;
-        unsigned long long* h = hist + t_ndoff[f] + slot * Qw;
+        unsigned long long* h = hist + t_ndoff[f] + slot * a.nd_stride;
         if constexpr (!(DLSA_CAT_ABLATE & 1)) {
           lds_add(h, w, a.hscale[0]);
 #pragma unroll
@@ -240,7 +240,8 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
   auto nd_sum = [&](int f, int lev, int col) {
     const int nl = a.nlev[f], R = a.nd_rep[f];
     long long s = 0;
-    for (int rp = 0; rp < R; ++rp) s += hist_at(hist, a.nd_off[f] + (rp * nl + lev) * Qw + col);
+    for (int rp = 0; rp < R; ++rp)
+      s += hist_at(hist, a.nd_off[f] + (rp * nl + lev) * a.nd_stride + col);
     return (double)s / (col == 0 ? a.hscale[0] : a.hscale[1 + col]);
   };
 

@@ -148,6 +148,8 @@ struct CatArgs {
   double* slab_ll;
   int32_t q, F, P, intercept, NT, want_phase;
   int32_t hist_doubles;       // LDS histogram doubles
+  int32_t nd_stride;          // 8-byte words per (replica, level) row of an nd histogram: q + 1
+                              // rounded up to odd (the lanes' rows then fall on distinct banks)
   int32_t nlev[kCatMaxFactors];    // dummy columns of factor f (L_f - 1)
   int32_t doff[kCatMaxFactors];    // parameter index of factor f's first dummy
   int32_t nd_off[kCatMaxFactors];  // LDS: [rep][nlev][q + 1] (w, w x_0 ..)
