@@ -16,11 +16,16 @@
 // columns that are neither active nor ignored, which is what lsa.py:157-161
 // computes whenever no variable has been ignored.
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 #include <xmmintrin.h>
 
 #include <algorithm>
+#include <atomic>
 #include <string>
+#include <functional>
+#include <memory>
+#include <thread>
 #include <vector>
 
 #include "../../include/dlsa_hip.h"
@@ -51,6 +56,49 @@ inline double dot(
   for (; i < n; ++i) s0 += x[i] * y[i];
   return (s0 + s1) + (s2 + s3);
 }
+
+// Spinning worker pool for the per-knot equiangular product a = Sigma[:, A] w
+// at large m (P = 500: ~half of the path's flops).  Thread t owns a fixed
+// column range and accumulates over the active set in the same order as the
+// serial loop, so the result is bit-identical for any thread count.  Workers
+// spin (no sleep) between the ~m knots of one path and exit with it.
+class SpinPool {
+ public:
+  template <typename F>
+  SpinPool(int n, F&& job) : n_(n) {
+    job_ = [job](int t) { job(t); };
+    for (int t = 1; t < n_; ++t) th_.emplace_back([this, t] { worker(t); });
+  }
+  ~SpinPool() {
+    stop_.store(true, std::memory_order_release);
+    gen_.fetch_add(1, std::memory_order_acq_rel);
+    for (auto& t : th_) t.join();
+  }
+  void run() {  // every thread runs job(t) once; returns when all are done
+    done_.store(0, std::memory_order_relaxed);
+    gen_.fetch_add(1, std::memory_order_acq_rel);
+    job_(0);
+    while (done_.load(std::memory_order_acquire) < n_ - 1) _mm_pause();
+  }
+
+ private:
+  void worker(int t) {
+    int seen = 0;
+    for (;;) {
+      int g;
+      while ((g = gen_.load(std::memory_order_acquire)) == seen) _mm_pause();
+      seen = g;
+      if (stop_.load(std::memory_order_acquire)) return;
+      job_(t);
+      done_.fetch_add(1, std::memory_order_acq_rel);
+    }
+  }
+  int n_;
+  std::function<void(int)> job_;
+  std::vector<std::thread> th_;
+  std::atomic<int> gen_{0}, done_{0};
+  std::atomic<bool> stop_{false};
+};
 
 struct Chol {
   // upper-triangular R (d x d) stored with leading dimension m
@@ -153,7 +201,22 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
   int rank = 0;
   int k = 0;
   std::vector<double> C, u, Gi1, w, a;
+  bool u_valid = false;
   std::vector<int> inactive, keep;
+  // threads for a = Sigma[:, A] w above m = 256 (DLSA_LARS_THREADS overrides,
+  // 1 = serial); column ranges are whole 8-double blocks
+  int nthr = m >= 256 ? std::min(8, (int)std::max(1u, std::thread::hardware_concurrency())) : 1;
+  if (const char* e = getenv("DLSA_LARS_THREADS")) nthr = std::max(1, std::min(32, atoi(e)));
+  std::unique_ptr<SpinPool> pool;
+  if (nthr > 1) {
+    pool.reset(new SpinPool(nthr, [&, nthr](int t) {
+      const int nb = (m + 7) / 8;
+      const int j0 = std::min(m, 8 * (nb * t / nthr)), j1 = std::min(m, 8 * (nb * (t + 1) / nthr));
+      const int na = (int)active.size();
+      for (int q = 0; q < na; ++q)
+        axpy(j1 - j0, w[q], &Sig[(size_t)active[q] * m + j0], a.data() + j0);
+    }));
+  }
 
   while (k < max_steps && (int)active.size() < m) {
     ++k;
@@ -201,10 +264,24 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
     }
     const int na = (int)active.size();
     if (na == 0) break;
-    // Gi1 = (R^T R)^-1 Sign ; A = 1/sqrt(Sign . Gi1) ; w = A Gi1
-    u.assign(na, 0.0);
+    // Gi1 = (R^T R)^-1 Sign ; A = 1/sqrt(Sign . Gi1) ; w = A Gi1.
+    // u = R^-T Sign is kept across knots: R^T is lower triangular, so adding
+    // a variable (a new last row of R^T, a new last entry of Sign) leaves the
+    // leading entries of u unchanged and only the new ones are computed, in
+    // the forward solve's own order (same rounding); a Givens downdate (lasso
+    // drop) rotates R and the whole u is recomputed.
+    if (!u_valid || (int)u.size() > na) {
+      u.assign(na, 0.0);
+      R.solve_rt(Sign.data(), u.data());
+      u_valid = true;
+    } else {
+      for (int i = (int)u.size(); i < na; ++i) {
+        double x = Sign[i];
+        for (int q = 0; q < i; ++q) x -= R.at(q, i) * u[q];
+        u.push_back(x / R.at(i, i));
+      }
+    }
     Gi1.assign(na, 0.0);
-    R.solve_rt(Sign.data(), u.data());
     R.solve_r(u.data(), Gi1.data());
     double sg = 0;
     for (int q = 0; q < na; ++q) sg += Gi1[q] * Sign[q];
@@ -216,8 +293,12 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
     // axpys (Sigma is symmetric): the equiangular correlations of every
     // column, used by the step length and by the correlation update
     a.assign(m, 0.0);
-    for (int q = 0; q < na; ++q)
-      axpy(m, w[q], &Sig[(size_t)active[q] * m], a.data());
+    if (pool) {
+      pool->run();
+    } else {
+      for (int q = 0; q < na; ++q)
+        axpy(m, w[q], &Sig[(size_t)active[q] * m], a.data());
+    }
     if (na < m) {
       keep.clear();
       for (int j = 0; j < m; ++j)
@@ -285,6 +366,7 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
         R.d = d - 1;
       }
       rank = R.d;
+      u_valid = false;
       std::vector<int> na_active;
       std::vector<double> na_sign;
       for (int q = 0; q < na; ++q) {
