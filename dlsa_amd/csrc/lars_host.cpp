@@ -21,11 +21,7 @@
 #include <xmmintrin.h>
 
 #include <algorithm>
-#include <atomic>
 #include <string>
-#include <functional>
-#include <memory>
-#include <thread>
 #include <vector>
 
 #include "../../include/dlsa_hip.h"
@@ -56,49 +52,6 @@ inline double dot(
   for (; i < n; ++i) s0 += x[i] * y[i];
   return (s0 + s1) + (s2 + s3);
 }
-
-// Spinning worker pool for the per-knot equiangular product a = Sigma[:, A] w
-// at large m (P = 500: ~half of the path's flops).  Thread t owns a fixed
-// column range and accumulates over the active set in the same order as the
-// serial loop, so the result is bit-identical for any thread count.  Workers
-// spin (no sleep) between the ~m knots of one path and exit with it.
-class SpinPool {
- public:
-  template <typename F>
-  SpinPool(int n, F&& job) : n_(n) {
-    job_ = [job](int t) { job(t); };
-    for (int t = 1; t < n_; ++t) th_.emplace_back([this, t] { worker(t); });
-  }
-  ~SpinPool() {
-    stop_.store(true, std::memory_order_release);
-    gen_.fetch_add(1, std::memory_order_acq_rel);
-    for (auto& t : th_) t.join();
-  }
-  void run() {  // every thread runs job(t) once; returns when all are done
-    done_.store(0, std::memory_order_relaxed);
-    gen_.fetch_add(1, std::memory_order_acq_rel);
-    job_(0);
-    while (done_.load(std::memory_order_acquire) < n_ - 1) _mm_pause();
-  }
-
- private:
-  void worker(int t) {
-    int seen = 0;
-    for (;;) {
-      int g;
-      while ((g = gen_.load(std::memory_order_acquire)) == seen) _mm_pause();
-      seen = g;
-      if (stop_.load(std::memory_order_acquire)) return;
-      job_(t);
-      done_.fetch_add(1, std::memory_order_acq_rel);
-    }
-  }
-  int n_;
-  std::function<void(int)> job_;
-  std::vector<std::thread> th_;
-  std::atomic<int> gen_{0}, done_{0};
-  std::atomic<bool> stop_{false};
-};
 
 struct Chol {
   // upper-triangular R (d x d) stored with leading dimension m
@@ -187,9 +140,13 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
   }
 
   const size_t rows = (size_t)max_steps + 1;
-  memset(beta_out, 0, sizeof(double) * rows * m);
-  std::vector<double> Csnap(rows * m);  // Cvec after each knot (knot 0: beta = 0)
-  memcpy(Csnap.data(), Cvec.data(), sizeof(double) * m);
+  // only the knots reached are written (row k is copied from row k-1 before
+  // its update): no memset of the max_steps x m output (16 MB at m = 500, and
+  // its page faults, cost more than the path itself)
+  memset(beta_out, 0, sizeof(double) * m);
+  std::vector<double> Csnap;  // Cvec after each knot (knot 0: beta = 0)
+  Csnap.reserve((size_t)std::min<size_t>(rows, 2 * (size_t)m + 2) * m);
+  Csnap.insert(Csnap.end(), Cvec.begin(), Cvec.end());
   auto B = [&](int k, int j) -> double& { return beta_out[(size_t)k * m + j]; };
 
   std::vector<int> active, ignores;
@@ -203,21 +160,6 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
   std::vector<double> C, u, Gi1, w, a;
   bool u_valid = false;
   std::vector<int> inactive, keep;
-  // threads for a = Sigma[:, A] w above m = 256 (DLSA_LARS_THREADS overrides,
-  // 1 = serial); column ranges are whole 8-double blocks
-  int nthr = m >= 256 ? std::min(8, (int)std::max(1u, std::thread::hardware_concurrency())) : 1;
-  if (const char* e = getenv("DLSA_LARS_THREADS")) nthr = std::max(1, std::min(32, atoi(e)));
-  std::unique_ptr<SpinPool> pool;
-  if (nthr > 1) {
-    pool.reset(new SpinPool(nthr, [&, nthr](int t) {
-      const int nb = (m + 7) / 8;
-      const int j0 = std::min(m, 8 * (nb * t / nthr)), j1 = std::min(m, 8 * (nb * (t + 1) / nthr));
-      const int na = (int)active.size();
-      for (int q = 0; q < na; ++q)
-        axpy(j1 - j0, w[q], &Sig[(size_t)active[q] * m + j0], a.data() + j0);
-    }));
-  }
-
   while (k < max_steps && (int)active.size() < m) {
     ++k;
     inactive.clear();
@@ -263,7 +205,11 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
       }
     }
     const int na = (int)active.size();
-    if (na == 0) break;
+    if (na == 0) {  // knot k stays the zero row (as with a pre-zeroed output)
+      memset(&B(k, 0), 0, sizeof(double) * m);
+      Csnap.resize((size_t)(k + 1) * m, 0.0);
+      break;
+    }
     // Gi1 = (R^T R)^-1 Sign ; A = 1/sqrt(Sign . Gi1) ; w = A Gi1.
     // u = R^-T Sign is kept across knots: R^T is lower triangular, so adding
     // a variable (a new last row of R^T, a new last entry of Sign) leaves the
@@ -293,12 +239,8 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
     // axpys (Sigma is symmetric): the equiangular correlations of every
     // column, used by the step length and by the correlation update
     a.assign(m, 0.0);
-    if (pool) {
-      pool->run();
-    } else {
-      for (int q = 0; q < na; ++q)
-        axpy(m, w[q], &Sig[(size_t)active[q] * m], a.data());
-    }
+    for (int q = 0; q < na; ++q)
+      axpy(m, w[q], &Sig[(size_t)active[q] * m], a.data());
     if (na < m) {
       keep.clear();
       for (int j = 0; j < m; ++j)
@@ -331,7 +273,7 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
     for (int j = 0; j < m; ++j) Cvec[j] -= gamhat * a[j];
     // Cvec = Sigma (sign b - beta_k): the knot's RSS is dff . Cvec (O(m)
     // instead of an O(m^2) quadratic form per knot at the end)
-    memcpy(&Csnap[(size_t)k * m], Cvec.data(), sizeof(double) * m);
+    Csnap.insert(Csnap.end(), Cvec.begin(), Cvec.end());  // row k
     if (lasso && any_drop) {
       for (int q = na - 1; q >= 0; --q) {
         if (!drops[q]) continue;
