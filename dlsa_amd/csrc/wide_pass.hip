@@ -977,23 +977,38 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
     __syncthreads();
     // trailing update A22 -= L21 L21^T on the lower 16x16 tiles (fp64 MFMA):
     // C[i][j] = sum_k Lp[16 ti + i][k] Lp[16 tj + j][k]
+    // UT tiles per wave at a time: their C reads are issued together, so one
+    // L2 / MALL latency covers UT read-modify-writes (the update is latency-
+    // bound: one CU per partition); tiles past the end recompute the last
+    // tile and skip the store
     const int m = rest / 16;
     const int ntiles = m * (m + 1) / 2;
-    for (int tt = wid; tt < ntiles; tt += 16) {
-      int ti, tj;
-      tile_ij(tt, ti, tj);
-      d4w acc = d4w{0, 0, 0, 0};
+    const int wv = __builtin_amdgcn_readfirstlane(wid);
+    constexpr int UT = 4;
+    for (int t0 = wv; t0 < ntiles; t0 += 16 * UT) {
+      int ti[UT], tj[UT];
+      d4w c[UT];
 #pragma unroll
-      for (int s = 0; s < CB / 4; ++s) {
-        const double av = Lp[(16 * ti + fl) * LDP + 4 * s + kq];
-        const double bv = Lp[(16 * tj + fl) * LDP + 4 * s + kq];
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+      for (int u = 0; u < UT; ++u) {
+        tile_ij(min(t0 + 16 * u, ntiles - 1), ti[u], tj[u]);
+        const double* cp = H + (int64_t)(jb + CB + 16 * ti[u] + kq) * PP + jb + CB + 16 * tj[u] + fl;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) c[u][r] = cp[4 * r * PP];
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = jb + CB + 16 * ti + kq + 4 * r;
-        const int jj = jb + CB + 16 * tj + fl;
-        H[(int64_t)i * PP + jj] -= acc[r];
+      for (int u = 0; u < UT; ++u) {
+        d4w acc = d4w{0, 0, 0, 0};
+#pragma unroll
+        for (int s = 0; s < CB / 4; ++s) {
+          const double av = Lp[(16 * ti[u] + fl) * LDP + 4 * s + kq];
+          const double bv = Lp[(16 * tj[u] + fl) * LDP + 4 * s + kq];
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+        }
+        if (t0 + 16 * u < ntiles) {
+          double* cp = H + (int64_t)(jb + CB + 16 * ti[u] + kq) * PP + jb + CB + 16 * tj[u] + fl;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) cp[4 * r * PP] = c[u][r] - acc[r];
+        }
       }
     }
     __syncthreads();
