@@ -166,28 +166,64 @@ constexpr int wave_w_default(int NT) { return (NT >= 2 && NT <= 7) ? 2 : 1; }
 constexpr int wave_lpr(int NT, int W) { return (W == 1 && NT <= 7) ? 4 : 8; }
 constexpr int wave_rb(int NT, int W) { return W * (64 / wave_lpr(NT, W)); }
 
-// tile rows of wave `wid`: lower-triangle row I holds I + 1 tiles; rows are
-// dealt largest first to the lighter wave (NT = 7: {6, 3, 2} and {5, 4, 1, 0},
-// 14 tiles each)
-constexpr unsigned wave_rows_mask(int NT, int W, int wid) {
+// Edge strip (DLSA_WAVE_STRIP, default on).  The last tile row holds only
+// s = P - 16 (NT - 1) parameter rows (4 at P = 100).  On the MI355X a
+// v_mfma_f64_16x16x4 issues every ~44 ns per SIMD, a v_mfma_f64_4x4x4_4b
+// every ~7 ns (tools/mfma4_probe.hip, profiles/r02_mfma4_probe.txt), so with
+// NS > 0 the strip's tiles are NS 4x4x4_4b sub-blocks each instead of one
+// 16x16x4 (NS = 1 for s <= 4, 2 for s <= 8).  4x4x4_4b maps (probe): A lane
+// i + 4 b + 16 k, B lane j + 4 b + 16 k, D lane j + 4 b + 16 i, block b
+// independent (CBSZ / ABID broadcasts have no effect on it), so the A operand
+// of sub-block r is feature 16 (NT - 1) + 4 r + (l & 3) of row k in every
+// block -- read from LDS -- and B is the 16x16x4 column operand unchanged:
+// D lane j + 4 b + 16 i = H[16 (NT - 1) + 4 r + i][16 J + 4 b + j].
+// (Computing every tile as 4x4x4_4b sub-blocks against DPP-rotated B -- the
+// probe's 75 TF/s shape -- measured slower in this kernel: 31.0 vs 29.3 ms per
+// config-2 exact pass, profiles/r02w_mf4_ab.txt.)
+#ifndef DLSA_WAVE_STRIP
+#define DLSA_WAVE_STRIP 1
+#endif
+constexpr int wave_strip_ns(int NT, int P) {
+  return (!DLSA_WAVE_STRIP || NT < 2) ? 0
+         : (P - 16 * (NT - 1) <= 4)   ? 1
+         : (P - 16 * (NT - 1) <= 8)   ? 2
+                                      : 0;
+}
+
+// MFMA time of tile row I in quarter tiles (a 4x4x4_4b ~ 1/4 of a 16x16x4
+// issue slot, conservatively)
+constexpr int wave_row_cost(int NT, int NS, int I) {
+  return (NS > 0 && I == NT - 1) ? NT * NS : 4 * (I + 1);
+}
+
+// tile rows of wave `wid`: rows are dealt most expensive first to the lighter
+// wave (NT = 7, no strip: {6, 3, 2} and {5, 4, 1, 0}, 14 tiles each; NS = 1:
+// {5, 2, 1} and {4, 3, 6, 0}, 44 / 47 quarter tiles)
+constexpr unsigned wave_rows_mask(int NT, int NS, int W, int wid) {
   if (W == 1) return (1u << NT) - 1;
   int load0 = 0, load1 = 0;
-  unsigned m0 = 0, m1 = 0;
-  for (int I = NT - 1; I >= 0; --I) {
+  unsigned m0 = 0, m1 = 0, done = 0;
+  for (int n = 0; n < NT; ++n) {
+    int best = -1;
+    for (int I = NT - 1; I >= 0; --I)
+      if (!((done >> I) & 1u) &&
+          (best < 0 || wave_row_cost(NT, NS, I) > wave_row_cost(NT, NS, best)))
+        best = I;
+    done |= 1u << best;
     if (load0 <= load1) {
-      load0 += I + 1;
-      m0 |= 1u << I;
+      load0 += wave_row_cost(NT, NS, best);
+      m0 |= 1u << best;
     } else {
-      load1 += I + 1;
-      m1 |= 1u << I;
+      load1 += wave_row_cost(NT, NS, best);
+      m1 |= 1u << best;
     }
   }
   return wid == 0 ? m0 : m1;
 }
 
-template <int NT, int W, int WID>
+template <int NT, int NS, int W, int WID>
 struct WaveTiles {
-  static constexpr unsigned RM = wave_rows_mask(NT, W, WID);
+  static constexpr unsigned RM = wave_rows_mask(NT, NS, W, WID);
   static constexpr int count() {
     int c = 0;
     for (int I = 0; I < NT; ++I)
@@ -249,9 +285,13 @@ struct WaveCtx {
 
 // The block loop + epilogue of wave WID (a separate code path per wave: no
 // branch merges of the accumulator arrays).
-template <int NT, int W, int WID, bool STD, int FAM>
+template <int NT, int NS, int W, int WID, bool STD, int FAM>
 __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, char* smem) {
-  using TL = WaveTiles<NT, W, WID>;
+  using TL = WaveTiles<NT, NS, W, WID>;
+  // strip tiles (the last tile row as NS 4x4x4_4b sub-blocks)
+  constexpr auto strip = [](int I) { return NS > 0 && I == NT - 1; };
+  constexpr bool HAS_STRIP = NS > 0 && ((TL::RM >> (NT - 1)) & 1u);
+  constexpr int NSA = NS > 0 ? NS : 1;
   constexpr int LPR = wave_lpr(NT, W);
   constexpr int RW = 64 / LPR;   // rows of a block in this wave's row phase
   constexpr int RB = W * RW;     // rows per block
@@ -274,9 +314,14 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
 #pragma unroll
   for (int m = 0; m < M; ++m) gacc[m] = 0.0;
   double llacc = 0.0;
-  wd4 acc[TW];
+  wd4 acc[TW];           // 16x16x4 tiles (AGPRs)
+  double sacc[TW][NSA];  // strip sub-blocks (the unused entries of either are dead)
 #pragma unroll
-  for (int i = 0; i < TW; ++i) acc[i] = wd4{0.0, 0.0, 0.0, 0.0};
+  for (int i = 0; i < TW; ++i) {
+    acc[i] = wd4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int r = 0; r < NSA; ++r) sacc[i][r] = 0.0;
+  }
 
   // DMA: wave WID issues pieces j = WID, WID + W, ...; the last wave also y
   int my_ops = 0;
@@ -359,11 +404,17 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
 
     // ---- tile phase: KS k-steps of 4 rows, this wave's TW tiles ---------------
     // operands of k-step s+1 are read while the MFMAs of k-step s run
-    double xo[2][NC], wk[2];
+    double xo[2][NC], xso[2][NSA], wk[2];
     auto load = [&](int s, int u) {
       const double* xq = xs + (4 * s + q) * p + (fl - ic);
 #pragma unroll
       for (int c = 0; c < NC; ++c) xo[u][c] = xq[16 * c];
+      if constexpr (HAS_STRIP) {
+        // strip A operand of sub-block r: feature 16 (NT - 1) + 4 r + (l & 3)
+        const double* xt = xq + 16 * (NT - 1) + (lane & 3) - fl;
+#pragma unroll
+        for (int r = 0; r < NS; ++r) xso[u][r] = xt[4 * r];
+      }
       wk[u] = wv[4 * s + q];
     };
     load(0, 0);
@@ -379,15 +430,31 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
         xv[c] = v;
         if ((TL::RM >> c) & 1u) av[c] = v * wk[u];
       }
+      double as[NSA];
+      if constexpr (HAS_STRIP) {
+#pragma unroll
+        for (int r = 0; r < NS; ++r) as[r] = xso[u][r] * wk[u];
+      }
       wv_static_for<TW>([&](auto iI) {
         constexpr int i = decltype(iI)::value;
         constexpr int I = TL::I_of(i), J = TL::J_of(i);
-        acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[I], xv[J], acc[i], 0, 0, 0);
+        if constexpr (strip(I)) {
+#pragma unroll
+          for (int r = 0; r < NS; ++r)
+            sacc[i][r] = __builtin_amdgcn_mfma_f64_4x4x4f64(as[r], xv[J], sacc[i][r], 0, 0, 0);
+        } else {
+          acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[I], xv[J], acc[i], 0, 0, 0);
+        }
       });
     }
-    // keep every accumulator in AGPRs across the loop back edge
-#pragma unroll
-    for (int i = 0; i < TW; ++i) asm volatile("" : "+a"(acc[i]));
+    // keep every 16x16x4 accumulator in AGPRs across the loop back edge (the
+    // strip's 64-bit ones are left to the allocator: pinned one by one they
+    // get shuffled between AGPRs; explicit capture: an asm operand alone does
+    // not capture in a generic lambda)
+    wv_static_for<TW>([&acc](auto iI) {
+      constexpr int i = decltype(iI)::value;
+      if constexpr (!(NS > 0 && TL::I_of(i) == NT - 1)) asm volatile("" : "+a"(acc[i]));
+    });
   }
   wv_wait_vmcnt<0>();
 
@@ -397,8 +464,14 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
     constexpr int i = decltype(iI)::value;
     constexpr int t = TL::I_of(i) * (TL::I_of(i) + 1) / 2 + TL::J_of(i);
 #pragma unroll
-    for (int r = 0; r < 4; ++r)  // f64 16x16x4 C/D map: row = (l >> 4) + 4 r, col = l & 15
-      sH[t * 256 + (q + 4 * r) * 16 + fl] = acc[i][r];
+    for (int r = 0; r < 4; ++r) {
+      if constexpr (strip(TL::I_of(i))) {
+        // sub-block r: rows 4 r + (l >> 4), columns l & 15; rows past it: 0
+        sH[t * 256 + (4 * r + q) * 16 + fl] = r < NS ? sacc[i][r < NSA ? r : 0] : 0.0;
+      } else {  // f64 16x16x4 C/D map: row = (l >> 4) + 4 r, col = l & 15
+        sH[t * 256 + (q + 4 * r) * 16 + fl] = acc[i][r];
+      }
+    }
   });
   // gradient: sum the RW row lanes of each feature group, then the W waves
 #pragma unroll
@@ -434,7 +507,7 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
   }
 }
 
-template <int NT, int W, bool STD, int FAM>
+template <int NT, int NS, int W, bool STD, int FAM>
 __global__ __launch_bounds__(64 * W, W == 1 ? 1 : 2) void irls_wave_kernel(const PassArgs a) {
   constexpr int RB = wave_rb(NT, W);
   constexpr int PMAX = 16 * NT;
@@ -480,12 +553,12 @@ __global__ __launch_bounds__(64 * W, W == 1 ? 1 : 2) void irls_wave_kernel(const
   cx.yr = wv_rsrc(ycb, a.y_last4 + 4 - ycb);
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   if constexpr (W == 1) {
-    wave_body<NT, 1, 0, STD, FAM>(a, cx, smem);
+    wave_body<NT, NS, 1, 0, STD, FAM>(a, cx, smem);
   } else {
     if (wid == 0)
-      wave_body<NT, W, 0, STD, FAM>(a, cx, smem);
+      wave_body<NT, NS, W, 0, STD, FAM>(a, cx, smem);
     else
-      wave_body<NT, W, 1, STD, FAM>(a, cx, smem);
+      wave_body<NT, NS, W, 1, STD, FAM>(a, cx, smem);
   }
 }
 
@@ -500,7 +573,19 @@ static inline int wave_w(int NT) {
 template <int NT, int W, bool STD, int FAM>
 static hipError_t launch_wave_t(const PassArgs& a, int n_chunks, hipStream_t s) {
   const size_t lds = wave_lds_bytes_impl(NT, wave_rb(NT, W), a.p);
-  hipLaunchKernelGGL((irls_wave_kernel<NT, W, STD, FAM>), dim3(n_chunks), dim3(64 * W), lds, s, a);
+  switch (wave_strip_ns(NT, a.P)) {
+    case 1:
+      hipLaunchKernelGGL((irls_wave_kernel<NT, 1, W, STD, FAM>), dim3(n_chunks), dim3(64 * W), lds,
+                         s, a);
+      break;
+    case 2:
+      hipLaunchKernelGGL((irls_wave_kernel<NT, 2, W, STD, FAM>), dim3(n_chunks), dim3(64 * W), lds,
+                         s, a);
+      break;
+    default:
+      hipLaunchKernelGGL((irls_wave_kernel<NT, 0, W, STD, FAM>), dim3(n_chunks), dim3(64 * W), lds,
+                         s, a);
+  }
   return hipGetLastError();
 }
 

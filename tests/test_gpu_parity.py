@@ -825,3 +825,35 @@ def test_logistic_model_eval_dummy_branch_vs_reference(golden_dir, torch_cuda, M
                             center=center, scale=scale)
     assert np.isfinite(out.to_numpy()).all()
     assert np.abs(out.to_numpy()[0] - ref).max() <= 1e-10 * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("p,fi,std", [(20, False, False), (24, False, False), (36, True, False),
+                                      (87, True, True), (100, True, False), (116, False, False)])
+def test_exact_pass_edge_strip_vs_oracle(torch_cuda, M, p, fi, std):
+    """The exact pass's last tile row as 4x4x4_4b sub-blocks (irls_wave_impl.hpp
+    edge strip): one sub-block (P - 16 (NT - 1) <= 4: P = 20, 116) and two
+    (<= 8: P = 24, 37, 88, 101), in the two-wave and the one-wave (NT = 8)
+    geometry, fp64 fits and OLS against the oracle."""
+    sizes = [2999, 1781, 4096 + 13]
+    n = sum(sizes)
+    X, y = O.simulate_counter(n, p, seed=5 * p + fi)
+    center = scale = None
+    if std:
+        X = X * 2.0 + 0.3
+        center, scale = X.mean(0), X.std(0)
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    fit = M.logistic_model_batched(X, y, off, fit_intercept=fi, center=center, scale=scale,
+                                   hessian="fp64", rows_per_chunk=1000)
+    th, S, St, ll, it = O.logistic_fit_partitions(X, y, off, fit_intercept=fi, center=center,
+                                                  scale=scale)
+    assert (fit.status.cpu().numpy() == 0).all()
+    assert _rel(fit.theta.cpu(), th) < REL
+    assert _rel(fit.sig_inv.cpu(), S) < REL
+    assert _rel(fit.sig_inv_theta.cpu(), St) < REL
+    assert _rel(fit.loglik.cpu(), ll) < 1e-10
+    yl = X[:, :3].sum(1) + 0.1 * y
+    ols = M.ols_model_batched(X, yl, off, fit_intercept=fi, rows_per_chunk=1000)
+    for k in range(3):
+        o = O.ols_fit(X[off[k]:off[k + 1]], yl[off[k]:off[k + 1]], fit_intercept=fi)
+        assert _rel(ols.theta[k].cpu(), o["coef"]) < REL
+        assert _rel(ols.sig_inv[k].cpu(), o["Sig_inv"]) < 1e-12
