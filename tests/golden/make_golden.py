@@ -437,8 +437,28 @@ def golden_eval():
     print("eval done:", rec["missing_level_outcome"])
 
 
+def golden_p100_k8():
+    """p = 100, K = 8, n_k = 2e4 (seed 7): per-partition frames
+    at tol 1e-12, WLSE / ONESHOT and the LASSO path of the reference."""
+    np.random.seed(7)
+    pid, lab, feat = simulate_logistic_arrays(160000, 100, "systematic", 8)
+    cols = ["x" + str(i) for i in range(100)]
+    df = pd.DataFrame(np.concatenate([pid[:, None], lab[:, None], feat], 1),
+                      columns=["partition_id", "label"] + cols)
+    outs = ref_map(df, "label", False, tol=1e-12)
+    wlse, oneshot, S = combine(outs, 8)
+    AIC, BIC, beta, _ = ref_lars(S, wlse, 160000, "lasso")
+    np.savez_compressed(os.path.join(OUT, "p100_n16e4_K8.npz"), seed=7, n=160000,
+                        p=100, K=8, checksum_X=float(feat.sum()),
+                        checksum_y=float(lab.sum()), outs=outs, wlse=wlse, oneshot=oneshot,
+                        lars_lasso_AIC=AIC, lars_lasso_BIC=BIC, lars_lasso_beta=beta)
+    print("p100 K8 done; support", np.nonzero(beta[int(np.argmin(BIC))])[0].size)
+
+
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "eval":
+    if len(sys.argv) > 1 and sys.argv[1] == "p100_k8":
+        golden_p100_k8()
+    elif len(sys.argv) > 1 and sys.argv[1] == "eval":
         golden_eval()
     elif len(sys.argv) > 1 and sys.argv[1] == "dummy":
         golden_dummy()
@@ -446,6 +466,7 @@ if __name__ == "__main__":
         golden_dummy_file()
     else:
         main()
+        golden_p100_k8()
         golden_dummy()
         golden_dummy_file()
         golden_eval()

@@ -70,12 +70,15 @@ def test_config1_vs_reference(golden_dir, torch_cuda, M, hessian, tag, fi):
         assert set(np.nonzero(sel["beta_byBIC"].to_numpy())[0]) == set(np.nonzero(gb)[0])
 
 
-def test_p100_vs_reference(golden_dir, torch_cuda, M):
+@pytest.mark.parametrize("name", ["p100_n8e4_K4.npz", "p100_n16e4_K8.npz"])
+def test_p100_vs_reference(golden_dir, torch_cuda, M, name):
+    """p = 100, n_k = 2e4, K = 4 and the SURVEY 8(c) K = 8 fixture."""
     from dlsa_amd.dlsa import dlsa, dlsa_mapred
 
-    P = _golden(golden_dir, "p100_n8e4_K4.npz")
+    P = _golden(golden_dir, name)
+    n, K = int(P["n"]), int(P["K"])
     np.random.seed(int(P["seed"]))
-    pid, lab, feat = O.simulate_logistic_arrays(80000, 100, "systematic", 4)
+    pid, lab, feat = O.simulate_logistic_arrays(n, 100, "systematic", K)
     order, off = O.systematic_partition(pid)
     fit = M.logistic_model_batched(feat[order], lab[order], off)
     assert (fit.status.cpu().numpy() == 0).all()
@@ -83,7 +86,7 @@ def test_p100_vs_reference(golden_dir, torch_cuda, M):
     assert _rel(fit.sig_inv.cpu(), P["outs"][:, :, 3:]) < REL
     comb = dlsa_mapred(fit)
     assert _rel(comb["beta_byOLS"], P["wlse"]) < REL
-    sel = dlsa(comb.iloc[:, 2:], comb["beta_byOLS"], 80000, type="lasso")
+    sel = dlsa(comb.iloc[:, 2:], comb["beta_byOLS"], n, type="lasso")
     gb = P["lars_lasso_beta"][int(np.argmin(P["lars_lasso_BIC"]))]
     assert set(np.nonzero(sel["beta_byBIC"].to_numpy())[0]) == set(np.nonzero(gb)[0])
 
