@@ -444,7 +444,8 @@ def main():
                                   "P^2+2P+2 fp64)"},
         "roofline": roof,
         "kernels": kern,
-        "stages_ms_per_step": {k: v / args.steps for k, v in stage_ms.items()},
+        "stages_ms_per_step": dict({k: v / args.steps for k, v in stage_ms.items()},
+                                   fit_native=tot("ms_total") / args.steps),
         "newton": {"iterations": last["iterations"], "passes_fp32": last["passes_fp32"],
                    "passes_fp64": last["passes_fp64"], "n_chunks": last["n_chunks"],
                    "status": fit.status_counts()},

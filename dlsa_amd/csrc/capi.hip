@@ -106,6 +106,24 @@ static std::vector<double> warm_level_fracs(bool fused) {
 // iteration budget of one warm-start level (its own, not part of max_iter)
 constexpr int kLevelIters = 10;
 // a level stops once its max relative step is below this; DLSA_LEVEL_TOL overrides
+// Pinned host staging of the per-iteration readbacks (running counters +
+// phases), grown on demand and kept for the thread's lifetime: a
+// hipHostMalloc / hipHostFree pair per fit costs a pinning call (and the free
+// an implicit synchronisation) on every call.  Never freed: the process exit
+// reclaims it (a thread_local destructor could run after the HIP runtime's).
+static int32_t* pinned_staging(size_t n_i32) {
+  thread_local int32_t* buf = nullptr;
+  thread_local size_t cap = 0;
+  if (cap < n_i32) {
+    int32_t* nb = nullptr;
+    if (hipHostMalloc((void**)&nb, n_i32 * 4, hipHostMallocDefault) != hipSuccess) return nullptr;
+    if (buf) (void)hipHostFree(buf);
+    buf = nb;
+    cap = n_i32;
+  }
+  return buf;
+}
+
 static double warm_level_tol(bool fused) {
   if (const char* e = getenv("DLSA_LEVEL_TOL")) return atof(e);
   return fused ? 0.2 : 0.1;
@@ -372,7 +390,7 @@ static std::vector<int64_t> plan_part_rows(const Plan& q, int K) {
     for (int c = q.part_chunk_begin[k]; c < q.part_chunk_begin[k + 1]; ++c) r[k] += q.chunk_rows[c];
   return r;
 }
-static int64_t phase_rows(const std::vector<int64_t>& part_rows, const std::vector<int32_t>& phase,
+static int64_t phase_rows(const std::vector<int64_t>& part_rows, const int32_t* phase,
                           int ph) {
   int64_t n = 0;
   for (size_t k = 0; k < part_rows.size(); ++k)
@@ -573,15 +591,12 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
   const bool standardize = center != nullptr;
   StreamTimer timed{stream, opt.record_timing != 0};
   DLSA_HIP_TRY(timed.init());
-  int32_t* h_cnt = nullptr;
-  DLSA_HIP_TRY(hipHostMalloc((void**)&h_cnt, 16, hipHostMallocDefault));
-  struct HFree {
-    int32_t* p;
-    ~HFree() {
-      if (p) (void)hipHostFree(p);
-    }
-  } hfree{h_cnt};
-  std::vector<int32_t> h_phase(K, 0);
+  int32_t* h_cnt = pinned_staging(4 + (size_t)K);
+  if (!h_cnt) {
+    set_error("pinned host staging allocation failed");
+    return DLSA_E_HIP;
+  }
+  int32_t* h_phase = h_cnt + 4;  // [K] phases (pinned: no staging copy per iteration)
 
   int it = 0;
   for (size_t lvl = 0; lvl < plans.size(); ++lvl) {
@@ -601,7 +616,7 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
                                       d_cnt, stream));
       DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, stream));
     }
-    DLSA_HIP_TRY(hipMemcpyAsync(h_phase.data(), d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
+    DLSA_HIP_TRY(hipMemcpyAsync(h_phase, d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
     DLSA_HIP_TRY(hipStreamSynchronize(stream));
     if (lvl > 0) {
       n_running[0] = h_cnt[0];
@@ -641,7 +656,7 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
       DLSA_HIP_TRY(timed(&g_stats.ms_solve,
                          [&] { return launch_wide_newton(sa, wa, d_rcb, d_gcb, d_H, K, stream); }));
       DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, stream));
-      DLSA_HIP_TRY(hipMemcpyAsync(h_phase.data(), d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
+      DLSA_HIP_TRY(hipMemcpyAsync(h_phase, d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
       DLSA_HIP_TRY(hipStreamSynchronize(stream));
       n_running[0] = h_cnt[0];
       n_running[1] = h_cnt[1];
@@ -848,17 +863,14 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
   const bool standardize = center != nullptr;
   StreamTimer timed{stream, opt.record_timing != 0};
 
-  int32_t* h_cnt = nullptr;
-  DLSA_HIP_TRY(hipHostMalloc((void**)&h_cnt, 16, hipHostMallocDefault));
-  struct HFree {
-    int32_t* p;
-    ~HFree() {
-      if (p) (void)hipHostFree(p);
-    }
-  } hfree{h_cnt};
+  int32_t* h_cnt = pinned_staging(4 + (size_t)K);
+  if (!h_cnt) {
+    set_error("pinned host staging allocation failed");
+    return DLSA_E_HIP;
+  }
 
   const bool trace = getenv("DLSA_TRACE") != nullptr;
-  std::vector<int32_t> h_phase(K, 0);
+  int32_t* h_phase = h_cnt + 4;  // [K] phases (pinned: no staging copy per iteration)
   int it = 0;
   for (size_t lvl = 0; lvl < plans.size(); ++lvl) {
     const Plan& q = plans[lvl];
@@ -871,7 +883,7 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
                                       d_cnt, stream));
       DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, stream));
     }
-    DLSA_HIP_TRY(hipMemcpyAsync(h_phase.data(), d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
+    DLSA_HIP_TRY(hipMemcpyAsync(h_phase, d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
     DLSA_HIP_TRY(hipStreamSynchronize(stream));
     if (lvl > 0) {
       n_running[0] = h_cnt[0];
@@ -908,7 +920,7 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
     DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
     DLSA_HIP_TRY(timed(&g_stats.ms_solve, [&] { return launch_newton_solve(sa, K, stream); }));
     DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, stream));
-    DLSA_HIP_TRY(hipMemcpyAsync(h_phase.data(), d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
+    DLSA_HIP_TRY(hipMemcpyAsync(h_phase, d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
     DLSA_HIP_TRY(hipStreamSynchronize(stream));
     n_running[0] = h_cnt[0];
     n_running[1] = h_cnt[1];
@@ -1223,14 +1235,11 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
 
   const bool standardize = center != nullptr;
   StreamTimer timed{stream, opt.record_timing != 0};
-  int32_t* h_cnt = nullptr;
-  DLSA_HIP_TRY(hipHostMalloc((void**)&h_cnt, 16, hipHostMallocDefault));
-  struct HFree {
-    int32_t* p;
-    ~HFree() {
-      if (p) (void)hipHostFree(p);
-    }
-  } hfree{h_cnt};
+  int32_t* h_cnt = pinned_staging(4 + (size_t)K);
+  if (!h_cnt) {
+    set_error("pinned host staging allocation failed");
+    return DLSA_E_HIP;
+  }
   const bool trace = getenv("DLSA_TRACE") != nullptr;
 
   int it = 0;
@@ -1257,7 +1266,7 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
       DLSA_HIP_TRY(timed(&g_stats.ms_pass_fp64,
                          [&] { return launch_cat_pass(ca, standardize, qn.n_chunks, stream); }));
       g_stats.passes_fp64++;
-      g_stats.rows_fp64 += phase_rows(part_rows, h_phase, PHASE_F64);
+      g_stats.rows_fp64 += phase_rows(part_rows, h_phase.data(), PHASE_F64);
       DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
       DLSA_HIP_TRY(timed(&g_stats.ms_solve, [&] { return launch_newton_solve(sa, K, stream); }));
       DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, stream));
