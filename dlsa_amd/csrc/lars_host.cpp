@@ -132,6 +132,23 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
     for (int j = 0; j < m; ++j) Sig[(size_t)i * m + j] *= absb[i] * absb[j];
   auto S = [&](int i, int j) { return Sig[(size_t)i * m + j]; };
 
+  // Sp: Sigma with its columns permuted so that the active set occupies the
+  // leading positions in `active` order (pos[j] = column position of
+  // variable j).  The equiangular correlations of an inactive column j are
+  // then one contiguous dot product Sp[j, 0..|A|) . w, and those of an active
+  // column are A * Sign exactly (Sigma_AA w = A Sigma_AA Sigma_AA^-1 Sign):
+  // (m - |A|) |A| multiply-adds per knot instead of m |A| strided row axpys
+  std::vector<double> Sp(Sig);
+  std::vector<int> perm(m), pos(m);
+  for (int j = 0; j < m; ++j) perm[j] = pos[j] = j;
+  auto swap_cols = [&](int p1, int p2) {
+    if (p1 == p2) return;
+    for (int i = 0; i < m; ++i) std::swap(Sp[(size_t)i * m + p1], Sp[(size_t)i * m + p2]);
+    std::swap(perm[p1], perm[p2]);
+    pos[perm[p1]] = p1;
+    pos[perm[p2]] = p2;
+  };
+
   std::vector<double> Cvec(m, 0.0);
   for (int j = 0; j < m; ++j) {
     double s = 0;
@@ -198,6 +215,7 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
           ignores.push_back(j);
           in_ignores[j] = 1;
         } else {
+          swap_cols(pos[j], (int)active.size());
           active.push_back(j);
           in_active[j] = 1;
           Sign.push_back((Cvec[j] > 0) - (Cvec[j] < 0));
@@ -235,12 +253,12 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
     w.assign(na, 0.0);
     for (int q = 0; q < na; ++q) w[q] = A * Gi1[q];
     double gamhat = Cmax / A;
-    // a = Sigma[:, active] w, accumulated over q in order as contiguous row
-    // axpys (Sigma is symmetric): the equiangular correlations of every
-    // column, used by the step length and by the correlation update
-    a.assign(m, 0.0);
-    for (int q = 0; q < na; ++q)
-      axpy(m, w[q], &Sig[(size_t)active[q] * m], a.data());
+    // a = Sigma[:, active] w: the equiangular correlations of every column,
+    // used by the step length and by the correlation update (see Sp)
+    a.resize(m);
+    for (int j = 0; j < m; ++j)
+      if (!in_active[j]) a[j] = dot(na, &Sp[(size_t)j * m], w.data());
+    for (int q = 0; q < na; ++q) a[active[q]] = A * Sign[q];
     if (na < m) {
       keep.clear();
       for (int j = 0; j < m; ++j)
@@ -322,6 +340,7 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
       }
       active.swap(na_active);
       Sign.swap(na_sign);
+      for (int q = 0; q < (int)active.size(); ++q) swap_cols(pos[active[q]], q);
     }
   }
 
