@@ -18,7 +18,7 @@
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
-#include <xmmintrin.h>
+#include <immintrin.h>
 
 #include <algorithm>
 #include <string>
@@ -53,11 +53,58 @@ inline double dot(
   return (s0 + s1) + (s2 + s3);
 }
 
+// out[j] = Sp[j, 0..n) . w for every j in rows: four rows per pass share
+// each load of w (AVX2 FMA, 2 accumulators per row)
+void dots_rows(int n, const double* Sp, size_t ld, const std::vector<int>& rows, const double* w,
+               double* out) {
+  size_t t = 0;
+  const int n8 = n & ~7;
+  for (; t + 4 <= rows.size(); t += 4) {
+    const double* r0 = Sp + (size_t)rows[t] * ld;
+    const double* r1 = Sp + (size_t)rows[t + 1] * ld;
+    const double* r2 = Sp + (size_t)rows[t + 2] * ld;
+    const double* r3 = Sp + (size_t)rows[t + 3] * ld;
+    __m256d a0 = _mm256_setzero_pd(), b0 = _mm256_setzero_pd();
+    __m256d a1 = _mm256_setzero_pd(), b1 = _mm256_setzero_pd();
+    __m256d a2 = _mm256_setzero_pd(), b2 = _mm256_setzero_pd();
+    __m256d a3 = _mm256_setzero_pd(), b3 = _mm256_setzero_pd();
+    for (int i = 0; i < n8; i += 8) {
+      const __m256d w0 = _mm256_loadu_pd(w + i), w1 = _mm256_loadu_pd(w + i + 4);
+      a0 = _mm256_fmadd_pd(_mm256_loadu_pd(r0 + i), w0, a0);
+      b0 = _mm256_fmadd_pd(_mm256_loadu_pd(r0 + i + 4), w1, b0);
+      a1 = _mm256_fmadd_pd(_mm256_loadu_pd(r1 + i), w0, a1);
+      b1 = _mm256_fmadd_pd(_mm256_loadu_pd(r1 + i + 4), w1, b1);
+      a2 = _mm256_fmadd_pd(_mm256_loadu_pd(r2 + i), w0, a2);
+      b2 = _mm256_fmadd_pd(_mm256_loadu_pd(r2 + i + 4), w1, b2);
+      a3 = _mm256_fmadd_pd(_mm256_loadu_pd(r3 + i), w0, a3);
+      b3 = _mm256_fmadd_pd(_mm256_loadu_pd(r3 + i + 4), w1, b3);
+    }
+    double s[4][4];
+    _mm256_storeu_pd(s[0], _mm256_add_pd(a0, b0));
+    _mm256_storeu_pd(s[1], _mm256_add_pd(a1, b1));
+    _mm256_storeu_pd(s[2], _mm256_add_pd(a2, b2));
+    _mm256_storeu_pd(s[3], _mm256_add_pd(a3, b3));
+    const double* rr[4] = {r0, r1, r2, r3};
+    for (int u = 0; u < 4; ++u) {
+      double v = (s[u][0] + s[u][1]) + (s[u][2] + s[u][3]);
+      for (int i = n8; i < n; ++i) v += rr[u][i] * w[i];
+      out[rows[t + u]] = v;
+    }
+  }
+  for (; t < rows.size(); ++t) out[rows[t]] = dot(n, Sp + (size_t)rows[t] * ld, w);
+}
+
 struct Chol {
-  // upper-triangular R (d x d) stored with leading dimension m
+  // upper-triangular R (d x d) stored with leading dimension m, and its
+  // transpose lt (row i of lt = column i of R) for the backward solve
   int m = 0, d = 0;
-  std::vector<double> r;
-  explicit Chol(int m_) : m(m_), d(0), r((size_t)m_ * m_, 0.0) {}
+  std::vector<double> r, lt;
+  explicit Chol(int m_) : m(m_), d(0), r((size_t)m_ * m_, 0.0), lt((size_t)m_ * m_, 0.0) {}
+  // after R changed other than by an appended column (Givens downdate)
+  void rebuild_lt() {
+    for (int i = 0; i < d; ++i)
+      for (int k = 0; k <= i; ++k) lt[(size_t)i * m + k] = r[(size_t)k * m + i];
+  }
   double& at(int i, int j) { return r[(size_t)i * m + j]; }
   double at(int i, int j) const { return r[(size_t)i * m + j]; }
   // solve R^T x = b (forward)
@@ -71,11 +118,16 @@ struct Chol {
       axpy(d - k - 1, -xk, &r[(size_t)k * m + k + 1], x + k + 1);
     }
   }
-  // solve R x = b (backward)
+  // solve R x = b (backward), column-oriented on lt: x[i] is final once the
+  // terms of x[i+1..d) are subtracted; each then updates x[0..i) with one
+  // contiguous axpy (no per-row horizontal reduction on the recurrence)
   void solve_r(const double* b, double* x) const {
+    for (int i = 0; i < d; ++i) x[i] = b[i];
     for (int i = d - 1; i >= 0; --i) {
-      const double* ri = &r[(size_t)i * m];
-      x[i] = (b[i] - dot(d - i - 1, ri + i + 1, x + i + 1)) / ri[i];
+      const double* li = &lt[(size_t)i * m];
+      const double xi = x[i] / li[i];
+      x[i] = xi;
+      axpy(i, -xi, li, x);
     }
   }
 };
@@ -192,6 +244,7 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
         if (da == 0) {
           R.d = 1;
           R.at(0, 0) = sqrt(S(j, j));
+          R.lt[0] = R.at(0, 0);
           rank = 1;
         } else {
           std::vector<double> xold(da), rcol(da);
@@ -208,6 +261,8 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
           for (int q = 0; q < da; ++q) R.at(q, da) = rcol[q];
           for (int q = 0; q < da; ++q) R.at(da, q) = 0.0;
           R.at(da, da) = rpp;
+          for (int q = 0; q < da; ++q) R.lt[(size_t)da * m + q] = rcol[q];
+          R.lt[(size_t)da * m + da] = rpp;
           R.d = da + 1;
         }
         if (rank == (int)active.size()) {  // singular: back out, ignore j
@@ -256,8 +311,10 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
     // a = Sigma[:, active] w: the equiangular correlations of every column,
     // used by the step length and by the correlation update (see Sp)
     a.resize(m);
+    inactive.clear();
     for (int j = 0; j < m; ++j)
-      if (!in_active[j]) a[j] = dot(na, &Sp[(size_t)j * m], w.data());
+      if (!in_active[j]) inactive.push_back(j);
+    dots_rows(na, Sp.data(), (size_t)m, inactive, w.data(), a.data());
     for (int q = 0; q < na; ++q) a[active[q]] = A * Sign[q];
     if (na < m) {
       keep.clear();
@@ -326,6 +383,7 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
         R.d = d - 1;
       }
       rank = R.d;
+      R.rebuild_lt();
       u_valid = false;
       std::vector<int> na_active;
       std::vector<double> na_sign;
