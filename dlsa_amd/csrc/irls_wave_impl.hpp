@@ -168,10 +168,11 @@ constexpr int wave_rb(int NT, int W) { return W * (64 / wave_lpr(NT, W)); }
 
 // Edge strip (DLSA_WAVE_STRIP, default on).  The last tile row holds only
 // s = P - 16 (NT - 1) parameter rows (4 at P = 100).  On the MI355X a
-// v_mfma_f64_16x16x4 issues every ~44 ns per SIMD, a v_mfma_f64_4x4x4_4b
-// every ~7 ns (tools/mfma4_probe.hip, profiles/r02_mfma4_probe.txt), so with
-// NS > 0 the strip's tiles are NS 4x4x4_4b sub-blocks each instead of one
-// 16x16x4 (NS = 1 for s <= 4, 2 for s <= 8).  4x4x4_4b maps (probe): A lane
+// v_mfma_f64_4x4x4_4b issues every ~7 ns per SIMD (75 TF/s chip-wide;
+// tools/mfma4_probe.hip, profiles/r02_mfma4_probe.txt) -- a quarter of a
+// 16x16x4's flops in a fraction of its issue time -- so with NS > 0 the
+// strip's tiles are NS 4x4x4_4b sub-blocks each instead of one 16x16x4
+// (NS = 1 for s <= 4, 2 for s <= 8).  4x4x4_4b maps (probe): A lane
 // i + 4 b + 16 k, B lane j + 4 b + 16 k, D lane j + 4 b + 16 i, block b
 // independent (CBSZ / ABID broadcasts have no effect on it), so the A operand
 // of sub-block r is feature 16 (NT - 1) + 4 r + (l & 3) of row k in every
