@@ -53,6 +53,10 @@ constexpr int RB = kCoopRows;   // rows per block
 #ifndef DLSA_ABLATE
 #define DLSA_ABLATE 0
 #endif
+// bf16 operands (round 2): ONE image Z = bf16(sqrt(w) x), H~ = Z^T Z (positive
+// semi-definite by construction, as in the wide fused pass), instead of the
+// two images x and w x -- half the image stores and LDS: 9.87 -> 9.37 ms per
+// config-2 launch (profiles/r02ac_zimage_ab.txt)
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -191,11 +195,11 @@ inline int coop_slot_bytes_impl(int NT, int p) {
 }
 
 // LDS beyond the ring: w, r of the block [2][RB] fp64, center / 1/scale
-// [2][PMAX] fp64, and the bf16 MFMA operands of the block: x and w*x,
-// [PMAX][RB + 16] bf16 each (feature-major, so one lane's 8 consecutive k are one
+// [2][PMAX] fp64, and the bf16 MFMA operand image of the block z = sqrt(w) x,
+// [PMAX][RB + 16] bf16 (feature-major, so one lane's 8 consecutive k are one
 // 16-byte read).
 inline int coop_extra_bytes_impl(int NT) {
-  return (2 * RB + 2 * 16 * NT) * 8 + 2 * 16 * NT * (RB + 16) * 2;
+  return (2 * RB + 2 * 16 * NT) * 8 + 16 * NT * (RB + 16) * 2;
 }
 
 // Tile phase of wave WID for one 32-row block.
@@ -209,27 +213,8 @@ __device__ __forceinline__ void tile_phase(Acc (&acc)[(CG<NT, W>::TPW)], const d
   const int fl = lane & 15, q = lane >> 4;
   const bool icpt_lane = ic && fl == 0;
   const double* xq = xs + q * p + (fl - ic);  // row q of the block, this lane's feature
-  if constexpr (PREC == PREC_BF16) {
-    // operands staged by the row phase: k index 8q + j = block row 8q + j
-    const __bf16* obw = obx + G::PMAX * G::OBS;
-    bf16x8 Bv[NT], Av[NT];
-    static_for<NT>([&](auto cI) {
-      constexpr int c = decltype(cI)::value;
-      if constexpr ((CM >> c) & 1u) {
-        const int o = (16 * c + fl) * G::OBS + 8 * q;
-        Bv[c] = *(const bf16x8*)(obx + o);
-        if constexpr ((RM >> c) & 1u) Av[c] = *(const bf16x8*)(obw + o);
-      }
-    });
-    static_for<G::TPW>([&](auto iI) {
-      constexpr int i = decltype(iI)::value;
-      constexpr int t = WID * G::TPW + i;
-      if constexpr (t < G::T) {
-        constexpr int I = tile_I(t), J = tile_J(t);
-        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Av[I], Bv[J], acc[i], 0, 0, 0);
-      }
-    });
-  } else {
+  static_assert(PREC != PREC_BF16, "bf16 tiles are issued by the kernel body");
+  {
     // 8 k-steps of 4 rows: k-step s uses block rows 4s + q (k = q)
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
@@ -449,23 +434,22 @@ void irls_coop_kernel(const PassArgs a) {
         wr[RB + rB] = r;
       }
       if constexpr (PREC == PREC_BF16) {
-        // stage the bf16 MFMA operands once per row (x and w*x)
-        const float wf = (float)w;
+        // stage the bf16 MFMA operand z = sqrt(w) x once per row; one
+        // v_cvt_pk_bf16_f32 converts two of the lane's features
+        const float swf = __builtin_sqrtf((float)w);
 #pragma unroll
-        for (int m = 0; m < M; ++m) {
-          const int o = (sl + LPR * m) * G::OBS + rB;
-          float xf = (float)xv[m];
-          // opaque to the optimiser: otherwise (bf16)(float)x is folded into a
-          // direct f64 -> bf16 conversion, lowered with round-to-odd fix-ups
-          // (6 extra VALU per value); x is finite, double rounding is harmless
-          asm volatile("" : "+v"(xf));
-          // one v_cvt_pk_bf16_f32 for x and w x; halves stored with
-          // ds_write_b16 / ds_write_b16_d16_hi
-          const f2c pr = {xf, xf * wf};
+        for (int m = 0; m < M; m += 2) {
+          float z0 = (float)xv[m];
+          float z1 = m + 1 < M ? (float)xv[m + 1] : 0.0f;
+          // opaque: otherwise (bf16)(float)x folds into a direct f64 -> bf16
+          // conversion with round-to-odd fix-ups
+          asm volatile("" : "+v"(z0), "+v"(z1));
+          const f2c pr = {z0 * swf, z1 * swf};
           const bf16x2c pk = __builtin_convertvector(pr, bf16x2c);
-          obx[o] = pk[0];
-          obx[G::PMAX * G::OBS + o] = pk[1];
+          obx[(sl + LPR * m) * G::OBS + rB] = pk[0];
+          if (m + 1 < M) obx[(sl + LPR * (m + 1)) * G::OBS + rB] = pk[1];
         }
+
       }
     }
     lds_barrier();  // B2: w, r (and the bf16 operand images) of all 32 rows visible
@@ -476,12 +460,11 @@ void irls_coop_kernel(const PassArgs a) {
         // one code path for every wave: the wave's tile indices are
         // wave-uniform registers (no per-wave copies of the loop body, whose
         // merge would copy the accumulators every block)
-        const __bf16* obw = obx + G::PMAX * G::OBS;
         const int fl = lane & 15, q = lane >> 4;
 #pragma unroll
         for (int i = 0; i < G::TPW; ++i) {
           if (wid * G::TPW + i < G::T) {  // wave-uniform
-            const bf16x8 Av = *(const bf16x8*)(obw + (16 * tI[i] + fl) * G::OBS + 8 * q);
+            const bf16x8 Av = *(const bf16x8*)(obx + (16 * tI[i] + fl) * G::OBS + 8 * q);
             const bf16x8 Bv = *(const bf16x8*)(obx + (16 * tJ[i] + fl) * G::OBS + 8 * q);
             acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Av, Bv, acc[i], 0, 0, 0);
           }
