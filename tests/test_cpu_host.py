@@ -92,6 +92,25 @@ def test_native_lars_vs_oracle_random(seed, intercept, typ):
     assert np.allclose(r["beta0"], o["beta0"], rtol=1e-10, atol=1e-10)
 
 
+def test_native_lars_vs_oracle_config5_size():
+    """LASSO path at the config-5 width class (m = 400, 401 knots): the native
+    path (permuted-Sigma equiangular products, transposed-R back solve) against
+    the oracle restatement of lsa.py:90-212, knot by knot."""
+    from dlsa_amd.lsa import lars_lsa
+
+    rs = np.random.RandomState(3)
+    m = 400
+    X = rs.rand(3000, m) - 0.5
+    S = X.T @ X
+    b = np.where(rs.rand(m) < 0.4, 1.0, 0.0) + 0.05 * rs.randn(m)
+    r = lars_lsa(S, b, False, 1e5, type="lasso")
+    o = O.lars_lsa(S, b, False, 1e5, type="lasso")
+    assert r["beta"].shape == o["beta"].shape
+    assert np.abs(r["beta"] - o["beta"]).max() < 1e-10 * max(1.0, np.abs(o["beta"]).max())
+    assert np.abs(r["BIC"] - o["BIC"]).max() < 1e-10 * np.abs(o["BIC"]).max()
+    assert int(np.argmin(r["BIC"])) == int(np.argmin(o["BIC"]))
+
+
 @pytest.mark.parametrize("fi", [False, True])
 def test_dlsa_selection_vs_oracle(golden_dir, fi):
     from dlsa_amd.dlsa import dlsa
