@@ -65,10 +65,14 @@ struct Plan {
 // (cooperative bf16 / fp64 pass ms): 1024 chunks 22.0 / 42.5, 2048 19.4 /
 // 36.6, 4096 18.2 / 34.7, 8192 17.4 / 33.2, 16384 17.0 / 32.8 (but the Newton
 // solve reads every chunk's partial tiles: 0.65 -> 0.74 ms per iteration).
+// Round 2: at least 4096 rows per chunk -- at the strong-scaling share of
+// config 2 (n = 1.25e7 per GPU, 1525 rows per chunk by the 8192 rule) chunks
+// of 3072 / 6144 rows fit 12.8 / 12.7 ms against 13.5 ms (fewer per-chunk
+// prologues and partial tiles; profiles/r02am_chunk_ab.txt).
 static int auto_rows_per_chunk(int64_t n_total) {
   if (const char* e = getenv("DLSA_ROWS_PER_CHUNK")) return std::max(64, atoi(e));
   int64_t r = n_total / 8192;
-  r = std::max<int64_t>(1024, std::min<int64_t>(r, 131072));
+  r = std::max<int64_t>(4096, std::min<int64_t>(r, 131072));
   return (int)r;
 }
 
