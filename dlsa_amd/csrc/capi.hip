@@ -65,13 +65,18 @@ struct Plan {
 // (cooperative bf16 / fp64 pass ms): 1024 chunks 22.0 / 42.5, 2048 19.4 /
 // 36.6, 4096 18.2 / 34.7, 8192 17.4 / 33.2, 16384 17.0 / 32.8 (but the Newton
 // solve reads every chunk's partial tiles: 0.65 -> 0.74 ms per iteration).
-// Round 2: at least 4096 rows per chunk -- at the strong-scaling share of
-// config 2 (n = 1.25e7 per GPU, 1525 rows per chunk by the 8192 rule) chunks
-// of 3072 / 6144 rows fit 12.8 / 12.7 ms against 13.5 ms (fewer per-chunk
-// prologues and partial tiles; profiles/r02am_chunk_ab.txt).
+// Round 2 (current kernels): ~6144 chunks of at least 4096 rows.  Config 2
+// at 16384 rows per chunk (6144 chunks) against the old 8448: 82.8-84.1 vs
+// 84.6-91.0 ms alternated on one box, 86.2-86.6 vs 86.3-86.6 on another
+// (profiles/r02ap_c2_chunk_ab.txt, r02ar_c2_chunk_ab.txt); at the
+// strong-scaling share of config 2 (n = 1.25e7 per GPU, 1525 rows per chunk
+// by the old rule) 3072 / 6144-row chunks fit 12.8 / 12.7 ms against 13.5 ms
+// (fewer per-chunk prologues and partial tiles; r02am).
 static int auto_rows_per_chunk(int64_t n_total) {
   if (const char* e = getenv("DLSA_ROWS_PER_CHUNK")) return std::max(64, atoi(e));
-  int64_t r = n_total / 8192;
+  // rounded up to a multiple of 1024: equal partitions then split into whole
+  // chunks (config 2: 16384 rows, 6 per partition) instead of a ragged extra one
+  int64_t r = (n_total / 6144 + 1023) / 1024 * 1024;
   r = std::max<int64_t>(4096, std::min<int64_t>(r, 131072));
   return (int)r;
 }
