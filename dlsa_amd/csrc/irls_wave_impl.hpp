@@ -87,8 +87,9 @@ __device__ __forceinline__ double wv_dpp(double v) {
 // commutative pair).
 template <int R>
 __device__ __forceinline__ double wv_row_sum(double v) {
-  static_assert(R == 16 || R == 8, "16 or 8 rows per block");
-  if constexpr (R == 8) v += wv_dpp<0x128>(v);  // row_ror 8: l ^ 8
+  static_assert(R == 16 || R == 8 || R == 4, "16, 8 or 4 rows per block");
+  if constexpr (R == 4) v += __shfl_xor(v, 4);   // l ^ 4 (no DPP form)
+  if constexpr (R <= 8) v += wv_dpp<0x128>(v);  // row_ror 8: l ^ 8
   v = wv_xor16(v);
   v = wv_xor32(v);
   return v;
@@ -162,9 +163,18 @@ __host__ __device__ __forceinline__ int wave_lds_bytes_impl(int NT, int RB, int 
 // split between the waves in the row phase (P >= 17).  W = 1 (P <= 128): all T tiles
 // in one wave, one wave per SIMD.  DLSA_WAVE_W overrides for profiling.
 constexpr int wave_w_default(int NT) { return (NT >= 2 && NT <= 7) ? 2 : 1; }
-// lanes per row in the row phase: 16 rows per wave at W = 1 (P <= 112), else 8
-constexpr int wave_lpr(int NT, int W) { return (W == 1 && NT <= 7) ? 4 : 8; }
-constexpr int wave_rb(int NT, int W) { return W * (64 / wave_lpr(NT, W)); }
+// Lanes per row in the row phase: 4 (16 rows per wave) at W = 1, P <= 112; 16 (4
+// rows per wave, 8-row blocks) for OLS at W = 2, P <= 64; else 8.  The OLS
+// setting halves the ring (12 vs 21 KB per workgroup at P = 64: LDS allowed only
+// 3.5 waves per SIMD) and runs 5 waves per SIMD (wave_min_waves): config-4 pass
+// 16.2 vs 17.4 ms (profiles/r02at_lpr_ab.txt).  Logistic keeps 8: its exp / rcp /
+// log sequence runs once per RW rows, and 4-row (or 16-row, RB = 32: 3.5 -> 2
+// waves per SIMD by LDS) blocks measured slower at P = 64 (4.3 / 4.8 vs 3.4 ms,
+// r02at / r02as).
+constexpr int wave_lpr(int NT, int W, int FAM) {
+  return (W > 1 && NT <= 4 && FAM == FAMILY_GAUSSIAN) ? 16 : (W == 1 && NT <= 7) ? 4 : 8;
+}
+constexpr int wave_rb(int NT, int W, int FAM) { return W * (64 / wave_lpr(NT, W, FAM)); }
 
 // Edge strip (DLSA_WAVE_STRIP, default on).  The last tile row holds only
 // s = P - 16 (NT - 1) parameter rows (4 at P = 100).  On the MI355X a
@@ -293,7 +303,7 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
   constexpr auto strip = [](int I) { return NS > 0 && I == NT - 1; };
   constexpr bool HAS_STRIP = NS > 0 && ((TL::RM >> (NT - 1)) & 1u);
   constexpr int NSA = NS > 0 ? NS : 1;
-  constexpr int LPR = wave_lpr(NT, W);
+  constexpr int LPR = wave_lpr(NT, W, FAM);
   constexpr int RW = 64 / LPR;   // rows of a block in this wave's row phase
   constexpr int RB = W * RW;     // rows per block
   constexpr int KS = RB / 4;     // MFMA k-steps per block
@@ -508,9 +518,16 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
   }
 }
 
+// minimum waves per SIMD (register budget): OLS at P <= 64 fits 5 (48 VGPRs +
+// <= 41 AGPRs, no scratch); the logistic kernels would spill there
+constexpr int wave_min_waves(int NT, int W, int FAM) {
+  return W == 1 ? 1 : (NT <= 4 && FAM == FAMILY_GAUSSIAN ? 5 : 2);
+}
+
 template <int NT, int NS, int W, bool STD, int FAM>
-__global__ __launch_bounds__(64 * W, W == 1 ? 1 : 2) void irls_wave_kernel(const PassArgs a) {
-  constexpr int RB = wave_rb(NT, W);
+__global__ __launch_bounds__(64 * W, wave_min_waves(NT, W, FAM)) void irls_wave_kernel(
+    const PassArgs a) {
+  constexpr int RB = wave_rb(NT, W, FAM);
   constexpr int PMAX = 16 * NT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -573,7 +590,7 @@ static inline int wave_w(int NT) {
 
 template <int NT, int W, bool STD, int FAM>
 static hipError_t launch_wave_t(const PassArgs& a, int n_chunks, hipStream_t s) {
-  const size_t lds = wave_lds_bytes_impl(NT, wave_rb(NT, W), a.p);
+  const size_t lds = wave_lds_bytes_impl(NT, wave_rb(NT, W, FAM), a.p);
   switch (wave_strip_ns(NT, a.P)) {
     case 1:
       hipLaunchKernelGGL((irls_wave_kernel<NT, 1, W, STD, FAM>), dim3(n_chunks), dim3(64 * W), lds,
