@@ -191,6 +191,12 @@ constexpr int wave_rb(int NT, int W, int FAM) { return W * (64 / wave_lpr(NT, W,
 // (Computing every tile as 4x4x4_4b sub-blocks against DPP-rotated B -- the
 // probe's 75 TF/s shape -- measured slower in this kernel: 31.0 vs 29.3 ms per
 // config-2 exact pass, profiles/r02w_mf4_ab.txt.)
+// OLS: the tile phase takes x itself as the A operand (no w * x multiplies;
+// padded rows are zeroed in the ring by the row phase): 16.2-16.4 vs
+// 16.4-16.5 ms per config-4 pass (profiles/r02av_ols_nomul_ab.txt)
+#ifndef DLSA_WAVE_OLS_NOMUL
+#define DLSA_WAVE_OLS_NOMUL 1
+#endif
 #ifndef DLSA_WAVE_STRIP
 #define DLSA_WAVE_STRIP 1
 #endif
@@ -310,6 +316,9 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
   constexpr int PMAX = 16 * NT;
   constexpr int M = PMAX / LPR;  // features per lane in the row phase
   constexpr int TW = TL::TW, NC = TL::NC;
+  // OLS (w in {0, 1}): A operands are x itself (padded rows zeroed in the ring,
+  // the intercept column = w)
+  constexpr bool OLS_NOMUL = DLSA_WAVE_OLS_NOMUL && FAM == FAMILY_GAUSSIAN;
 
   const int lane = threadIdx.x & 63;
   const int p = a.p, P = a.P, ic = a.intercept;
@@ -380,6 +389,12 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
           // the intercept slot f = 0 is the previous row's last value)
           if (f >= ic && f < P) xrw[LPR * m] = v;
         }
+        if constexpr (OLS_NOMUL) {
+          // OLS: w is 1 on rows of the chunk and 0 past it; zero the padded
+          // rows' features in place so the tile phase can skip w * x
+          const int f = sl + LPR * m;
+          if (!valid && f >= ic && f < P) xrw[LPR * m] = 0.0;
+        }
         if (m == 0 && ic && sl == 0) v = 1.0;
         xv[m] = v;
         const double bm = bet[sl + LPR * m];
@@ -437,14 +452,14 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         double v = xo[u][c];
-        if (c == 0 && icpt_lane) v = 1.0;
+        if (c == 0 && icpt_lane) v = OLS_NOMUL ? wk[u] : 1.0;
         xv[c] = v;
-        if ((TL::RM >> c) & 1u) av[c] = v * wk[u];
+        if ((TL::RM >> c) & 1u) av[c] = OLS_NOMUL ? v : v * wk[u];
       }
       double as[NSA];
       if constexpr (HAS_STRIP) {
 #pragma unroll
-        for (int r = 0; r < NS; ++r) as[r] = xso[u][r] * wk[u];
+        for (int r = 0; r < NS; ++r) as[r] = OLS_NOMUL ? xso[u][r] : xso[u][r] * wk[u];
       }
       wv_static_for<TW>([&](auto iI) {
         constexpr int i = decltype(iI)::value;
