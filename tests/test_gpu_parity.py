@@ -281,6 +281,31 @@ def test_ols_vs_oracle(torch_cuda, M, p, fi):
         assert abs(fit.loglik[k].item() - rss) < 1e-6 * rss
 
 
+@pytest.mark.parametrize("p,fi,std", [(63, True, False), (40, True, True), (30, False, True),
+                                      (64, False, True)])
+def test_ols_small_p_geometry_vs_oracle(torch_cuda, M, p, fi, std):
+    """OLS at P <= 64 (16 lanes per row, 8-row blocks, x itself as the MFMA A
+    operand with the ring's padded rows zeroed and the intercept column = w):
+    ragged partitions and chunks (rows not a multiple of 8), with and without
+    the intercept and standardisation, against the oracle on the same design."""
+    rs = np.random.RandomState(100 + p)
+    sizes = [3001, 2045, 4093]
+    n = sum(sizes)
+    X = rs.rand(n, p) * 4.0 - 1.0
+    y = X @ rs.randn(p) + 0.7 + 0.1 * rs.randn(n)
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    center = X.mean(0) if std else None
+    scale = X.std(0) if std else None
+    fit = M.ols_model_batched(X, y, off, fit_intercept=fi, center=center, scale=scale,
+                              rows_per_chunk=1003)
+    assert (fit.status.cpu().numpy() == 0).all()
+    Xs = (X - center) / scale if std else X
+    for k in range(3):
+        o = O.ols_fit(Xs[off[k]:off[k + 1]], y[off[k]:off[k + 1]], fit_intercept=fi)
+        assert _rel(fit.theta[k].cpu(), o["coef"]) < REL
+        assert _rel(fit.sig_inv[k].cpu(), o["Sig_inv"]) < 1e-12
+
+
 @pytest.mark.parametrize("p,fi,std", [(10, False, False), (100, True, False), (37, True, True)])
 def test_loglik_eval_vs_oracle(torch_cuda, M, p, fi, std):
     """Evaluation pass (models.py:151-225): per-partition log-likelihood of 4
