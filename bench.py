@@ -2,9 +2,14 @@
 """DLSA logistic fit benchmark (BASELINE.json metric, config 2 by default).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
-                    [--scaling weak|strong]
+                    [--scaling strong|weak] [--backend nccl|gloo]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
+
+``--gpus N`` with N > 1 and no torchrun environment starts the N ranks itself:
+the launcher process (which never touches the GPU) runs torch.distributed.run
+as a child process with the same arguments and exits with its code.  Every
+rank checks that the process group holds exactly N ranks.
 
 One step = one complete DLSA fit of the GPU's shard: batched Newton/IRLS over
 all partitions (approximate-Hessian passes + the final fp64 pass whose Hessian
@@ -13,10 +18,11 @@ P^2+2P+2 sums (Sig_inv, Sig_inv theta, theta, K, N) across ranks, WLSE solve,
 LARS path and DBIC selection on the host.  Data are synthetic, generated in
 HBM by the counter-based generator before the timed region.
 
-Configs (BASELINE.json "configs"); sizes per GPU under weak
-scaling (the default), or of the whole job under --scaling strong (rank r
-then owns partitions [rK/N, (r+1)K/N) of the same global data set, SURVEY
-8(e)):
+Configs (BASELINE.json "configs"); sizes of the whole job under
+--scaling strong (the default: rank r owns partitions [rK/N, (r+1)K/N) of the
+same global data set; config 2 is then north_star's "n=1e8,
+p=100, 1024 partitions on 8 GPUs"), or per GPU under --scaling weak (at N = 1
+the two are the same workload):
   2  logistic n = 1e8, p = 100, K = 1024            (default; the headline metric)
   3  logistic n = 1.5e7, p = 181 + intercept, K = 128 (airline-like dummy-coded design;
                                                      1.2e8 rows on 8 GPUs)
@@ -96,6 +102,33 @@ def _cpu_worker(jobs, family, data, barrier, t_done, idx):
         t_done[idx] = time.time()
 
 
+def host_cores():
+    """CPUs this process may use: the affinity mask, capped by a cgroup CPU
+    quota (cpu.max / cfs_quota_us) when one is set.  Returns (cores, info)."""
+    import math
+
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = nproc
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    cores = aff if quota is None else max(1, min(aff, int(math.ceil(quota))))
+    return cores, {"nproc": nproc, "affinity": aff, "cgroup_cpu_quota": quota}
+
+
 def cpu_baseline(nk, p, n_parts, workers, family, seed=2019, data="counter"):
     """Oracle (port) timed on host cores: n_parts partitions of nk rows dealt
     to `workers` processes (1 BLAS thread each).  Every worker generates its
@@ -164,9 +197,12 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="weak: the config's n and K per GPU; strong: n and K of the whole job, "
-                         "partitions sharded over the ranks")
+    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
+                    help="strong (default): n and K of the whole job, partitions sharded over "
+                         "the ranks; weak: the config's n and K per GPU")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group transport for N > 1 (nccl = RCCL over xGMI; gloo: "
+                         "host transport, lets several ranks share one GPU in tests)")
     ap.add_argument("--n", type=int, default=0, help="rows (per GPU, or total when strong)")
     ap.add_argument("--p", type=int, default=0)
     ap.add_argument("--partitions", type=int, default=0)
@@ -181,6 +217,8 @@ def main():
                     help="config 3: categorical-code layout (LDS-histogram pass) or the dense "
                          "dummy-coded design")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     cfg = dict(CONFIGS[args.config])
     for key, v in (("n", args.n), ("p", args.p), ("K", args.partitions)):
         if v:
@@ -193,10 +231,24 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE = {world}")
+    ndev = torch.cuda.device_count()
+    if ndev < 1:
+        raise SystemExit("bench.py: no GPU visible")
+    if args.backend == "nccl" and world > ndev:
+        raise SystemExit(f"bench.py: {world} RCCL ranks need {world} GPUs ({ndev} visible); "
+                         "--backend gloo lets ranks share a GPU")
+    torch.cuda.set_device(local % ndev)
+    dev = torch.device("cuda", local % ndev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"bench.py: process group has {dist.get_world_size()} ranks, "
+                             f"--gpus {args.gpus}")
 
     from dlsa_amd import _hip
     from dlsa_amd.distributed import combine
@@ -289,7 +341,8 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     assert K_red == K_job and n_red == n_job, (K_red, n_red, K_job, n_job)
@@ -440,8 +493,10 @@ def main():
                    "family": family,
                    "hessian": args.hessian if family == "logistic" and not codes_layout else "fp64",
                    "tol": args.tol,
-                   "parallelism": f"dp{world} (partitions sharded; 1 RCCL all-reduce of "
-                                  "P^2+2P+2 fp64)"},
+                   "parallelism": f"dp{world} (partitions sharded; 1 "
+                                  f"{'RCCL' if args.backend == 'nccl' else 'gloo'} all-reduce of "
+                                  "P^2+2P+2 fp64)",
+                   "backend": args.backend if world > 1 else None},
         "roofline": roof,
         "kernels": kern,
         "stages_ms_per_step": dict({k: v / args.steps for k, v in stage_ms.items()},
@@ -461,18 +516,37 @@ def main():
         out["parity_sample"] = (f"partitions {smp} of rank 0 vs the numpy oracle (tol 1e-12): "
                                 "max |diff| / max |ref| over theta and Sig_inv")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        workers = min(16, os.cpu_count() or 1)
+        workers, cinfo = host_cores()      # every core this process may use
         if args.config == 5:
             nk_cpu, parts = 20000, 16      # ~8 s of single-thread work per partition
         else:                              # ~10-30 s of single-thread work in all
             nk_cpu, parts = n // K, {2: 32, 3: 32, 4: 128}[args.config]
-        parts = args.cpu_parts or parts
+        parts = args.cpu_parts or max(parts, 2 * workers)  # >= 2 partitions per core
         out["cpu_baseline"] = cpu_baseline(nk_cpu, p, parts, workers, family, data=data)
+        out["cpu_baseline"].update(cinfo)
         out["vs_cpu_baseline"] = value / out["cpu_baseline"]["value"]
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def launch_ranks(n):
+    """N ranks on this node without an external launcher: torch.distributed.run
+    as a CHILD process (this process never initialises the GPU, so no exec
+    from a GPU process), same arguments, rendezvous on 127.0.0.1 and a free
+    port.  Returns the child's exit code."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 if __name__ == "__main__":

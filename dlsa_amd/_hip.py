@@ -58,6 +58,8 @@ class FitStats(ctypes.Structure):
         ("ms_wide_row", ctypes.c_double),
         ("ms_wide_gram", ctypes.c_double),
         ("ms_wide_assemble", ctypes.c_double),
+        ("passes_f32x", ctypes.c_int32),
+        ("polish_partitions", ctypes.c_int32),
     ]
 
     def as_dict(self):

@@ -61,6 +61,26 @@ hipError_t launch_level_reset(int K, int P, int start_phase, int32_t* phase, int
   return hipGetLastError();
 }
 
+// Polish pass of a budget that ran out: every still-running partition gets
+// one exact pass at the theta it returns, whose X^T W X is published as
+// Sig_inv -- models.py:114,130 evaluate the weights at whatever coef sklearn
+// stopped at.  counters[PHASE_F64] = partitions marked.
+__global__ void polish_mark_kernel(int K, int32_t* phase, const int32_t* status,
+                                   int32_t* counters) {
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < K; k += gridDim.x * blockDim.x) {
+    if (status[k] != STATUS_RUNNING) continue;
+    phase[k] = PHASE_F64;
+    atomicAdd(&counters[PHASE_F64], 1);
+  }
+}
+
+hipError_t launch_polish_mark(int K, int32_t* phase, const int32_t* status, int32_t* counters,
+                              hipStream_t s) {
+  hipLaunchKernelGGL(polish_mark_kernel, dim3((K + 255) / 256), dim3(256), 0, s, K, phase, status,
+                     counters);
+  return hipGetLastError();
+}
+
 // sig_inv_theta = Sig_inv @ theta (models.py:131); still-running -> MAXITER.
 __global__ void fit_finalize_kernel(int K, int P, const double* theta, const double* sig_inv,
                                     double* sig_inv_theta, int32_t* status) {

@@ -112,8 +112,16 @@ static std::vector<double> warm_level_fracs(bool fused) {
   }
   return f;
 }
-// iteration budget of one warm-start level (its own, not part of max_iter)
+// iteration budget of one warm-start level: at most kLevelIters and at most
+// half of what is left of max_iter, so the levels and the full-data level
+// together run at most max_iter iterations (sklearn's n_iter_ <= max_iter)
+// and the full-data level always gets at least one; max_iter = 1 runs no
+// level at all.
 constexpr int kLevelIters = 10;
+static int iter_budget(bool final_level, int it, int max_iter) {
+  if (final_level) return std::max(1, max_iter - it);
+  return std::min(kLevelIters, (max_iter - it) / 2);
+}
 // a level stops once its max relative step is below this; DLSA_LEVEL_TOL overrides
 // Pinned host staging of the per-iteration readbacks (running counters +
 // phases), grown on demand and kept for the thread's lifetime: a
@@ -181,6 +189,7 @@ struct Layout {
   int64_t off_row0, off_rows, off_part, off_pcb, off_offsets;
   int64_t off_slabH, off_slabg, off_slabll;
   int64_t off_phase, off_bt, off_llprev, off_thprev, off_dprev, off_counters;
+  int64_t off_dmprev, off_stall;
   int64_t total;
 };
 
@@ -206,6 +215,8 @@ static Layout make_layout(const Plan& pl, int K) {
   L.off_thprev = take(8LL * K * pl.P);
   L.off_dprev = take(8LL * K * pl.P);
   L.off_counters = take(16);
+  L.off_dmprev = take(8LL * K);
+  L.off_stall = take(4LL * K);
   L.total = o;
   return L;
 }
@@ -248,6 +259,7 @@ struct WideLayout {
   int64_t off_g_row0, off_g_rows, off_g_part, off_gcb;
   int64_t off_offsets, off_w, off_slabg, off_slabll, off_slabG, off_slabgz, off_slabllz, off_H;
   int64_t off_phase, off_bt, off_llprev, off_thprev, off_dprev, off_counters;
+  int64_t off_dmprev, off_stall;
   int64_t total;
   int64_t cap_rows, cap_gram;  // row-chunk / Gram-row-group capacity of the tables and slabs
 };
@@ -295,6 +307,8 @@ static WideLayout make_wide_layout(const std::vector<WidePlans>& plans, int K, i
   L.off_thprev = take(8LL * K * P);
   L.off_dprev = take(8LL * K * P);
   L.off_counters = take(16);
+  L.off_dmprev = take(8LL * K);
+  L.off_stall = take(4LL * K);
   L.total = o;
   L.cap_rows = nr;
   L.cap_gram = ng;
@@ -409,6 +423,12 @@ static int64_t phase_rows(const std::vector<int64_t>& part_rows, const int32_t* 
 
 // DLSA_TRACE=1: per-iteration max |step| over all partitions (diagnostics;
 // copies theta and the last step to the host, so only for investigation)
+static int running_total(const int* n_running) {
+  int n = 0;
+  for (int ph = 0; ph < kRunPhases; ++ph) n += n_running[ph];
+  return n;
+}
+
 static hipError_t trace_iteration(int K, int P, const double* theta, const double* dprev,
                                   size_t lvl, int it, const int* n_running) {
   std::vector<double> th((size_t)K * P), dp((size_t)K * P);
@@ -421,8 +441,9 @@ static hipError_t trace_iteration(int K, int P, const double* theta, const doubl
     tmax = std::max(tmax, std::fabs(th[i]));
   }
   fprintf(stderr,
-          "[dlsa trace] level %zu iter %d: max|step| %.3e max|theta| %.3e running f32 %d f64 %d\n",
-          lvl, it, dmax, tmax, n_running[0], n_running[1]);
+          "[dlsa trace] level %zu iter %d: max|step| %.3e max|theta| %.3e running approx %d "
+          "f32x %d f64 %d\n",
+          lvl, it, dmax, tmax, n_running[PHASE_F32], n_running[PHASE_F32X], n_running[PHASE_F64]);
   return hipSuccess;
 }
 
@@ -575,13 +596,16 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
       (opt.hessian_mode == DLSA_HESSIAN_FP64 || family == FAMILY_GAUSSIAN) ? PHASE_F64 : PHASE_F32;
   DLSA_HIP_TRY(launch_fit_init(d_offsets, K, P, start_phase, theta, d_phase, d_bt, iters, status,
                                d_llprev, sig_inv, loglik, stream));
-  int n_running[2] = {0, 0};
+  int n_running[kRunPhases] = {0, 0, 0};
   for (int k = 0; k < K; ++k)
     if (offsets[k + 1] > offsets[k]) n_running[start_phase]++;
 
   SolveArgs sa;
   memset(&sa, 0, sizeof(sa));
   sa.theta = theta;
+  sa.dm_prev = (double*)at(L.off_dmprev);
+  sa.stall = (int32_t*)at(L.off_stall);
+  sa.escalate_to = PHASE_F64;  // no fp32 fused wide pass: bf16 -> fp64
   sa.theta_prev = (double*)at(L.off_thprev);
   sa.delta_prev = (double*)at(L.off_dprev);
   sa.ll_prev = d_llprev;
@@ -627,18 +651,16 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
     }
     DLSA_HIP_TRY(hipMemcpyAsync(h_phase, d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
     DLSA_HIP_TRY(hipStreamSynchronize(stream));
-    if (lvl > 0) {
-      n_running[0] = h_cnt[0];
-      n_running[1] = h_cnt[1];
-    }
+    if (lvl > 0)
+      for (int ph = 0; ph < kRunPhases; ++ph) n_running[ph] = h_cnt[ph];
     sa.subsample = final_level ? 0 : 1;
     sa.level_tol = warm_level_tol(false);
     sa.switch_tol = final_level ? opt.switch_tol : 0.0;
-    // a warm-start level has its own budget of kLevelIters iterations; the
-    // full-data level always gets max_iter (so a small max_iter still ends
-    // with full-row passes and a published Sig_inv)
-    const int it_end = it + (final_level ? max_iter : kLevelIters);
-    for (; it < it_end && (n_running[0] + n_running[1]) > 0 && q.rows.n_chunks > 0; ++it) {
+    const int it_end = it + iter_budget(final_level, it, max_iter);
+    if (it_end <= it) continue;  // no budget left for this warm-start level
+    DLSA_HIP_TRY(hipMemsetAsync(sa.dm_prev, 0, 8LL * K, stream));
+    DLSA_HIP_TRY(hipMemsetAsync(sa.stall, 0, 4LL * K, stream));
+    for (; it < it_end && running_total(n_running) > 0 && q.rows.n_chunks > 0; ++it) {
       // approximate partitions: one fused pass (gradient + bf16 Hessian)
       if (n_running[PHASE_F32] > 0) {
         DLSA_HIP_TRY(timed(
@@ -661,19 +683,43 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
       DLSA_HIP_TRY(timed(&g_stats.ms_wide_assemble,
                          [&] { return launch_wide_assemble(wa, d_gcb, d_H, K, stream); }));
       DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
-      sa.last_iter = it + 1 == it_end ? 1 : 0;
       DLSA_HIP_TRY(timed(&g_stats.ms_solve,
                          [&] { return launch_wide_newton(sa, wa, d_rcb, d_gcb, d_H, K, stream); }));
       DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, stream));
       DLSA_HIP_TRY(hipMemcpyAsync(h_phase, d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
       DLSA_HIP_TRY(hipStreamSynchronize(stream));
-      n_running[0] = h_cnt[0];
-      n_running[1] = h_cnt[1];
+      for (int ph = 0; ph < kRunPhases; ++ph) n_running[ph] = h_cnt[ph];
       if (getenv("DLSA_TRACE"))
         DLSA_HIP_TRY(trace_iteration(K, P, theta, sa.delta_prev, lvl, it, n_running));
     }
   }
   g_stats.iterations = it;
+  // polish: partitions the budget left running get Sig_inv = X^T W X at the
+  // theta they return (row pass + fp64 Gram pass, no step)
+  if (family == FAMILY_LOGISTIC && running_total(n_running) > 0 && plans.back().rows.n_chunks > 0) {
+    const WidePlans& q = plans.back();
+    DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
+    DLSA_HIP_TRY(launch_polish_mark(K, d_phase, status, d_cnt, stream));
+    DLSA_HIP_TRY(hipMemcpyAsync(h_phase, d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
+    DLSA_HIP_TRY(hipStreamSynchronize(stream));
+    const std::vector<int64_t> part_rows = plan_part_rows(q.rows, K);
+    DLSA_HIP_TRY(timed(&g_stats.ms_wide_row, [&] {
+      return launch_wide_row(wa, standardize, family, q.rows.n_chunks, stream);
+    }));
+    DLSA_HIP_TRY(timed(
+        &g_stats.ms_wide_gram, [&] { return launch_wide_gram(wa, standardize, stream); },
+        &g_stats.ms_pass_fp64));
+    g_stats.passes_fp64++;
+    g_stats.rows_fp64 += phase_rows(part_rows, h_phase, PHASE_F64);
+    g_stats.polish_partitions = running_total(n_running);
+    DLSA_HIP_TRY(timed(&g_stats.ms_wide_assemble,
+                       [&] { return launch_wide_assemble(wa, d_gcb, d_H, K, stream); }));
+    sa.eval_only = 1;
+    sa.subsample = 0;
+    DLSA_HIP_TRY(timed(&g_stats.ms_solve,
+                       [&] { return launch_wide_newton(sa, wa, d_rcb, d_gcb, d_H, K, stream); }));
+    sa.eval_only = 0;
+  }
   DLSA_HIP_TRY(launch_fit_finalize(K, P, theta, sig_inv, sig_inv_theta, status, stream));
   DLSA_HIP_TRY(hipStreamSynchronize(stream));
   g_stats.ms_total =
@@ -808,7 +854,7 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
   DLSA_HIP_TRY(launch_fit_init(d_offsets, K, P, start_phase, theta, d_phase, d_bt, iters, status,
                                d_llprev, sig_inv, loglik, stream));
 
-  int n_running[2] = {0, 0};
+  int n_running[kRunPhases] = {0, 0, 0};
   for (int k = 0; k < K; ++k)
     if (offsets[k + 1] > offsets[k]) n_running[start_phase]++;
 
@@ -868,6 +914,10 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
   sa.family = family;
   sa.tol = tol;
   sa.switch_tol = opt.switch_tol;
+  sa.dm_prev = (double*)at(L.off_dmprev);
+  sa.stall = (int32_t*)at(L.off_stall);
+  // a stalled bf16-steered partition goes on with fp32-MFMA Hessians first
+  sa.escalate_to = approx_prec == PREC_BF16 ? PHASE_F32X : PHASE_F64;
 
   const bool standardize = center != nullptr;
   StreamTimer timed{stream, opt.record_timing != 0};
@@ -880,6 +930,30 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
 
   const bool trace = getenv("DLSA_TRACE") != nullptr;
   int32_t* h_phase = h_cnt + 4;  // [K] phases (pinned: no staging copy per iteration)
+  // one pass over the chunks of plan q whose partition is in phase ph:
+  // exact (fp64 Hessian) passes by the per-wave kernel up to P = 128 and the
+  // cooperative one above; approximate passes (PHASE_F32 at the fit's
+  // approximate precision, PHASE_F32X at fp32) by the cooperative kernel
+  auto fused_pass = [&](int ph, const Plan& q, const std::vector<int64_t>& part_rows,
+                        const int32_t* hph) -> hipError_t {
+    const bool f64 = ph == PHASE_F64;
+    const int prec = f64 ? PREC_F64 : (ph == PHASE_F32X ? PREC_F32 : approx_prec);
+    pa.want_phase = ph;
+    const bool wave = f64 && q.NT <= kWaveMaxNT;
+    hipError_t e = timed(f64 ? &g_stats.ms_pass_fp64 : &g_stats.ms_pass_fp32, [&] {
+      if (wave) return launch_irls_wave(pa, q.NT, standardize, family, q.n_chunks, stream);
+      return launch_irls_coop(pa, q.NT, prec, standardize, family, q.n_chunks, stream);
+    });
+    if (f64) {
+      g_stats.passes_fp64++;
+      g_stats.rows_fp64 += phase_rows(part_rows, hph, ph);
+    } else {
+      g_stats.passes_fp32++;
+      g_stats.rows_fp32 += phase_rows(part_rows, hph, ph);
+      if (ph == PHASE_F32X) g_stats.passes_f32x++;
+    }
+    return e;
+  };
   int it = 0;
   for (size_t lvl = 0; lvl < plans.size(); ++lvl) {
     const Plan& q = plans[lvl];
@@ -894,49 +968,50 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
     }
     DLSA_HIP_TRY(hipMemcpyAsync(h_phase, d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
     DLSA_HIP_TRY(hipStreamSynchronize(stream));
-    if (lvl > 0) {
-      n_running[0] = h_cnt[0];
-      n_running[1] = h_cnt[1];
-    }
+    if (lvl > 0)
+      for (int ph = 0; ph < kRunPhases; ++ph) n_running[ph] = h_cnt[ph];
     sa.subsample = final_level ? 0 : 1;
     // the prefix MLE is ~sqrt(P/n) from the full one (max step ~0.35 entering
     // the full level at config 2), so a level need not converge: it stops at
     // a 0.2-relative step (warm_level_tol)
     sa.level_tol = warm_level_tol(true);
     sa.switch_tol = final_level ? opt.switch_tol : 0.0;
-    const int it_end = it + (final_level ? max_iter : kLevelIters);  // see fit_wide
-  for (; it < it_end && (n_running[0] + n_running[1]) > 0 && q.n_chunks > 0; ++it) {
-    for (int ph = 0; ph < 2; ++ph) {
-      if (n_running[ph] == 0) continue;
-      const bool f64 = ph == PHASE_F64;
-      pa.want_phase = ph;
-      // exact (fp64 Hessian) passes: the per-wave kernel up to P = 128, the
-      // cooperative one above; approximate passes: the cooperative kernel
-      const bool wave = f64 && q.NT <= kWaveMaxNT;
-      DLSA_HIP_TRY(timed(f64 ? &g_stats.ms_pass_fp64 : &g_stats.ms_pass_fp32, [&] {
-        if (wave) return launch_irls_wave(pa, q.NT, standardize, family, q.n_chunks, stream);
-        return launch_irls_coop(pa, q.NT, f64 ? PREC_F64 : approx_prec, standardize, family,
-                                q.n_chunks, stream);
-      }));
-      if (f64) {
-        g_stats.passes_fp64++;
-        g_stats.rows_fp64 += phase_rows(part_rows, h_phase, ph);
-      } else {
-        g_stats.passes_fp32++;
-        g_stats.rows_fp32 += phase_rows(part_rows, h_phase, ph);
+    const int it_end = it + iter_budget(final_level, it, max_iter);
+    if (it_end <= it) continue;  // no budget left for this warm-start level
+    DLSA_HIP_TRY(hipMemsetAsync(sa.dm_prev, 0, 8LL * K, stream));
+    DLSA_HIP_TRY(hipMemsetAsync(sa.stall, 0, 4LL * K, stream));
+    for (; it < it_end && running_total(n_running) > 0 && q.n_chunks > 0; ++it) {
+      // approximate (bf16 or fp32), escalated fp32, then exact passes
+      for (int ph : {PHASE_F32, PHASE_F32X, PHASE_F64}) {
+        if (n_running[ph] == 0) continue;
+        DLSA_HIP_TRY(fused_pass(ph, q, part_rows, h_phase));
       }
+      DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
+      DLSA_HIP_TRY(timed(&g_stats.ms_solve, [&] { return launch_newton_solve(sa, K, stream); }));
+      DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, stream));
+      DLSA_HIP_TRY(hipMemcpyAsync(h_phase, d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
+      DLSA_HIP_TRY(hipStreamSynchronize(stream));
+      for (int ph = 0; ph < kRunPhases; ++ph) n_running[ph] = h_cnt[ph];
+      if (trace) DLSA_HIP_TRY(trace_iteration(K, P, theta, d_dprev, lvl, it, n_running));
     }
-    DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
-    DLSA_HIP_TRY(timed(&g_stats.ms_solve, [&] { return launch_newton_solve(sa, K, stream); }));
-    DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, stream));
-    DLSA_HIP_TRY(hipMemcpyAsync(h_phase, d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
-    DLSA_HIP_TRY(hipStreamSynchronize(stream));
-    n_running[0] = h_cnt[0];
-    n_running[1] = h_cnt[1];
-    if (trace) DLSA_HIP_TRY(trace_iteration(K, P, theta, d_dprev, lvl, it, n_running));
-  }
   }
   g_stats.iterations = it;
+  // polish: partitions the budget left running (any phase) get one exact pass
+  // at the theta they return; its X^T W X is published as Sig_inv, no step
+  // (models.py:114,130 evaluate the weights at the coef sklearn stopped at)
+  if (family == FAMILY_LOGISTIC && running_total(n_running) > 0 && pl.n_chunks > 0) {
+    if (plans.size() > 1) DLSA_HIP_TRY(upload(pl));  // (already the last level's plan)
+    DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
+    DLSA_HIP_TRY(launch_polish_mark(K, d_phase, status, d_cnt, stream));
+    DLSA_HIP_TRY(hipMemcpyAsync(h_phase, d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
+    DLSA_HIP_TRY(hipStreamSynchronize(stream));
+    g_stats.polish_partitions = running_total(n_running);
+    DLSA_HIP_TRY(fused_pass(PHASE_F64, pl, plan_part_rows(pl, K), h_phase));
+    sa.eval_only = 1;
+    sa.subsample = 0;
+    DLSA_HIP_TRY(timed(&g_stats.ms_solve, [&] { return launch_newton_solve(sa, K, stream); }));
+    sa.eval_only = 0;
+  }
 
   DLSA_HIP_TRY(launch_fit_finalize(K, P, theta, sig_inv, sig_inv_theta, status, stream));
   DLSA_HIP_TRY(hipStreamSynchronize(stream));
@@ -1241,6 +1316,9 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
   sa.NT = pl.NT;
   sa.family = FAMILY_LOGISTIC;
   sa.tol = tol;
+  sa.dm_prev = (double*)at(L.off_dmprev);
+  sa.stall = (int32_t*)at(L.off_stall);
+  sa.escalate_to = PHASE_F64;  // every categorical pass is exact
 
   const bool standardize = center != nullptr;
   StreamTimer timed{stream, opt.record_timing != 0};
@@ -1265,12 +1343,13 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
       DLSA_HIP_TRY(hipMemcpyAsync(h_phase.data(), d_phase, 4LL * K, hipMemcpyDeviceToHost,
                                   stream));
       DLSA_HIP_TRY(hipStreamSynchronize(stream));
-      n_running = h_cnt[0] + h_cnt[1];
+      n_running = h_cnt[0] + h_cnt[1] + h_cnt[2];
     }
     sa.subsample = final_level ? 0 : 1;
     sa.level_tol = warm_level_tol(true);
     sa.switch_tol = 0.0;
-    const int it_end = it + (final_level ? max_iter : kLevelIters);  // see fit_wide
+    const int it_end = it + iter_budget(final_level, it, max_iter);
+    if (it_end <= it) continue;  // no budget left for this warm-start level
     for (; it < it_end && n_running > 0 && qn.n_chunks > 0; ++it) {
       DLSA_HIP_TRY(timed(&g_stats.ms_pass_fp64,
                          [&] { return launch_cat_pass(ca, standardize, qn.n_chunks, stream); }));
@@ -1282,12 +1361,26 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
       DLSA_HIP_TRY(hipMemcpyAsync(h_phase.data(), d_phase, 4LL * K, hipMemcpyDeviceToHost,
                                   stream));
       DLSA_HIP_TRY(hipStreamSynchronize(stream));
-      n_running = h_cnt[0] + h_cnt[1];
-      int nr[2] = {h_cnt[0], h_cnt[1]};
+      n_running = h_cnt[0] + h_cnt[1] + h_cnt[2];
+      int nr[kRunPhases] = {h_cnt[0], h_cnt[1], h_cnt[2]};
       if (trace) DLSA_HIP_TRY(trace_iteration(K, P, theta, sa.delta_prev, lvl, it, nr));
     }
   }
   g_stats.iterations = it;
+  // polish: Sig_inv of a partition the budget left running at the theta it
+  // returns (one more exact pass, no step; see fit_impl)
+  if (n_running > 0 && pl.n_chunks > 0) {
+    if (plans.size() > 1) DLSA_HIP_TRY(upload(pl));
+    DLSA_HIP_TRY(timed(&g_stats.ms_pass_fp64,
+                       [&] { return launch_cat_pass(ca, standardize, pl.n_chunks, stream); }));
+    g_stats.passes_fp64++;
+    g_stats.rows_fp64 += phase_rows(plan_part_rows(pl, K), h_phase.data(), PHASE_F64);
+    g_stats.polish_partitions = n_running;
+    sa.eval_only = 1;
+    sa.subsample = 0;
+    DLSA_HIP_TRY(timed(&g_stats.ms_solve, [&] { return launch_newton_solve(sa, K, stream); }));
+    sa.eval_only = 0;
+  }
   DLSA_HIP_TRY(launch_fit_finalize(K, P, theta, sig_inv, sig_inv_theta, status, stream));
   DLSA_HIP_TRY(hipStreamSynchronize(stream));
   g_stats.ms_total =

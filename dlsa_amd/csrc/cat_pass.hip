@@ -329,7 +329,10 @@ __global__ __launch_bounds__(256) void cat_presence_kernel(const CatArgs a, int3
     const double* xr = a.Xn + (row0 + r) * a.q;
 #pragma unroll
     for (int i = 0; i < kCatQMax; ++i)
-      if (i < a.q) mx[i] = fmax(mx[i], fabs(xr[i]));  // NaN-ignoring: a NaN row fails the fit later
+      // finite values only: a NaN / Inf row fails its own partition (non-finite
+      // log-likelihood) and must not widen the shared fixed-point grid of the
+      // column for every other partition
+      if (i < a.q && isfinite(xr[i])) mx[i] = fmax(mx[i], fabs(xr[i]));
   }
   // max is order-free: wave butterfly, then the 4 waves
 #pragma unroll

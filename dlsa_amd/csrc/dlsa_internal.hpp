@@ -10,11 +10,22 @@
 
 namespace dlsa {
 
-// Per-partition Newton phase.  MIXED fits start in PHASE_F32 (fp32-MFMA
-// Hessian, fp64 gradient) and switch to PHASE_F64 for the pass whose Hessian
-// is returned as Sig_inv; FP64 fits start in PHASE_F64.
+// Per-partition Newton phase.  MIXED fits start in PHASE_F32 (approximate
+// Hessian at the fit's approximate precision: bf16 MFMA in MIXED, fp32 in
+// MIXED_F32; fp64 gradient) and switch to PHASE_F64 for the pass whose
+// Hessian is returned as Sig_inv; FP64 fits start in PHASE_F64.  A partition
+// whose bf16-steered Newton stalls (or whose bf16 Hessian is not positive
+// definite) escalates to PHASE_F32X (fp32-MFMA Hessian), then to PHASE_F64.
 // PHASE_LEVEL_DONE: finished the current warm-start subsample level.
-enum : int32_t { PHASE_F32 = 0, PHASE_F64 = 1, PHASE_DONE = 2, PHASE_LEVEL_DONE = 3 };
+// counters[PHASE_F32 .. PHASE_F32X] count the partitions running per phase.
+enum : int32_t {
+  PHASE_F32 = 0,
+  PHASE_F64 = 1,
+  PHASE_F32X = 2,
+  PHASE_DONE = 3,
+  PHASE_LEVEL_DONE = 4
+};
+constexpr int kRunPhases = 3;
 enum : int32_t { STATUS_RUNNING = -1 };
 enum : int32_t { FAMILY_LOGISTIC = 0, FAMILY_GAUSSIAN = 1 };
 
@@ -68,7 +79,9 @@ struct SolveArgs {
   int32_t* backtracks;  // [K]
   int32_t* iters;       // [K]
   int32_t* status;      // [K]
-  int32_t* counters;    // [2] partitions still running per phase
+  int32_t* counters;    // [kRunPhases] partitions still running per phase
+  double* dm_prev;      // [K] max |step| of the last approximate iteration (0: none)
+  int32_t* stall;       // [K] consecutive stalled approximate iterations
   double* sig_inv;      // [K, P, P] out
   double* loglik;       // [K] out
   int32_t P;
@@ -78,8 +91,32 @@ struct SolveArgs {
   double tol;
   double switch_tol;
   double level_tol;   // warm-start level: stop when max|step| <= level_tol (1+max|theta|)
-  int32_t last_iter;  // wide path: the last iteration of the budget (publish Sig_inv)
+  int32_t escalate_to;  // next phase of a stalled PHASE_F32 partition (PHASE_F32X / PHASE_F64)
+  int32_t eval_only;    // polish: publish Sig_inv / loglik at the current theta, no step
 };
+
+// Stall detection of the approximate phases (newton_solve.hip,
+// wide_pass.hip).  With an approximate Hessian H~ and the exact gradient,
+// Newton contracts at rate ~ ||I - H~^-1 H|| (about kappa 2^-8 for bf16): on
+// an ill-conditioned design that rate nears 1 and the fit would crawl to
+// max_iter.  An approximate iteration "stalls" when its max |step| did not at
+// least halve against the previous one, or when it backtracks; two stalls in
+// a row move the partition one precision up (F32 -> escalate_to, F32X ->
+// F64).  Returns the phase to continue in.
+__device__ __forceinline__ int32_t escalate_phase(const SolveArgs& a, int32_t ph) {
+  return ph == PHASE_F32 ? a.escalate_to : PHASE_F64;
+}
+__device__ __forceinline__ int32_t approx_stall_step(const SolveArgs& a, int k, int32_t ph,
+                                                     bool stalled) {
+  const int st = stalled ? a.stall[k] + 1 : 0;
+  if (st >= 2) {
+    a.stall[k] = 0;
+    a.dm_prev[k] = 0.0;
+    return escalate_phase(a, ph);
+  }
+  a.stall[k] = st;
+  return ph;
+}
 
 // Arguments of the log-likelihood evaluation pass.
 struct EvalArgs {
@@ -215,6 +252,8 @@ hipError_t launch_fit_init(const int64_t* offsets_dev, int K, int P, int start_p
 hipError_t launch_level_reset(int K, int P, int start_phase, int32_t* phase, int32_t* status,
                               double* ll_prev, int32_t* backtracks, double* theta,
                               int32_t* counters, hipStream_t s);
+hipError_t launch_polish_mark(int K, int32_t* phase, const int32_t* status, int32_t* counters,
+                              hipStream_t s);
 hipError_t launch_fit_finalize(int K, int P, const double* theta, const double* sig_inv,
                                double* sig_inv_theta, int32_t* status, hipStream_t s);
 hipError_t launch_reduce_partitions(const double* sig_inv, const double* sig_inv_theta,

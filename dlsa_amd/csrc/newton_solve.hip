@@ -11,7 +11,9 @@
 //   3. publish H as Sig_inv (models.py:130: the information at the point the
 //      pass was evaluated) and the log-likelihood;
 //   4. Cholesky H = L L^T in LDS, solve L L^T d = g, theta += d;
-//   5. convergence / phase switch (fp32-MFMA Hessian -> fp64 pass).
+//   5. convergence / phase switch (approximate Hessian -> fp64 pass), stall
+//      escalation (bf16 -> fp32 -> fp64, dlsa_internal.hpp).
+// eval_only (the polish pass after a budget ran out): steps 1 and 3 only.
 #include <math.h>
 
 #include "dlsa_internal.hpp"
@@ -145,8 +147,8 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
   //    threshold above the fp32-log noise of mixed-mode log-likelihoods; real
   //    overshoots of a Newton step lose far more than 1e-6 relative
   const double llp = a.ll_prev[k];
-  if (a.family == FAMILY_LOGISTIC && it > 0 && ll < llp - 1e-6 * (1.0 + fabs(llp)) &&
-      a.backtracks[k] < 40) {
+  if (!a.eval_only && a.family == FAMILY_LOGISTIC && it > 0 &&
+      ll < llp - 1e-6 * (1.0 + fabs(llp)) && a.backtracks[k] < 40) {
     const int bt = a.backtracks[k] + 1;
     const double sc = ldexp(1.0, -bt);
     const double* tp = a.theta_prev + (int64_t)k * P;
@@ -155,7 +157,12 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
     if (tid == 0) {
       a.backtracks[k] = bt;
       a.iters[k] = it + 1;
-      atomicAdd(&a.counters[phase], 1);
+      int ph = phase;
+      if (!a.subsample && ph != PHASE_F64) {  // an approximate step that overshot
+        ph = approx_stall_step(a, k, ph, true);
+        a.phase[k] = ph;
+      }
+      atomicAdd(&a.counters[ph], 1);
     }
     return;
   }
@@ -170,6 +177,7 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
     }
     if (tid == 0) a.loglik[k] = ll;
   }
+  if (a.eval_only) return;  // polish: Sig_inv at the returned theta, no step
   __syncthreads();
 
   // 4. Cholesky, blocked (16-column panels), lower, in place in the packed
@@ -277,11 +285,15 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
       return;
     }
     if (tid == 0) {
-      if (phase == PHASE_F32 && a.family == FAMILY_LOGISTIC) {
-        // low-precision Hessian lost definiteness: redo this point with fp64
-        a.phase[k] = PHASE_F64;
+      if (phase != PHASE_F64 && a.family == FAMILY_LOGISTIC) {
+        // low-precision Hessian lost definiteness: redo this point one
+        // precision up (bf16 -> fp32 -> fp64)
+        const int32_t ph = escalate_phase(a, phase);
+        a.phase[k] = ph;
         a.iters[k] = it + 1;
-        atomicAdd(&a.counters[PHASE_F64], 1);
+        a.stall[k] = 0;
+        a.dm_prev[k] = 0.0;
+        atomicAdd(&a.counters[ph], 1);
       } else {
         a.status[k] = DLSA_STATUS_SINGULAR;
       }
@@ -435,8 +447,14 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
       a.status[k] = DLSA_STATUS_NONFINITE;
       return;
     }
-    if (ph == PHASE_F32) {
-      if (dm <= a.switch_tol * (1.0 + tm)) ph = PHASE_F64;
+    if (ph != PHASE_F64) {
+      if (dm <= a.switch_tol * (1.0 + tm)) {
+        ph = PHASE_F64;
+      } else {
+        const double dp = a.dm_prev[k];
+        ph = approx_stall_step(a, k, ph, dp > 0.0 && dm > 0.5 * dp);
+        if (ph == phase) a.dm_prev[k] = dm;
+      }
     } else if (dm <= a.tol * (1.0 + tm)) {
       a.status[k] = DLSA_STATUS_OK;
       a.phase[k] = PHASE_DONE;

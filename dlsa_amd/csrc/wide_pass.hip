@@ -884,8 +884,8 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
   }
   // 2. step halving on a log-likelihood decrease (newton_solve.hip step 2)
   const double llp = a.ll_prev[k];
-  if (a.family == FAMILY_LOGISTIC && it > 0 && ll < llp - 1e-6 * (1.0 + fabs(llp)) &&
-      a.backtracks[k] < 40) {
+  if (!a.eval_only && a.family == FAMILY_LOGISTIC && it > 0 &&
+      ll < llp - 1e-6 * (1.0 + fabs(llp)) && a.backtracks[k] < 40) {
     const int bt = a.backtracks[k] + 1;
     const double sc = ldexp(1.0, -bt);
     const double* tp = a.theta_prev + (int64_t)k * P;
@@ -894,16 +894,22 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
     if (tid == 0) {
       a.backtracks[k] = bt;
       a.iters[k] = it + 1;
-      atomicAdd(&a.counters[phase], 1);
+      int ph = phase;
+      if (!a.subsample && ph != PHASE_F64) {  // an approximate step that overshot
+        ph = approx_stall_step(a, k, ph, true);
+        a.phase[k] = ph;
+      }
+      atomicAdd(&a.counters[ph], 1);
     }
     return;
   }
-  // 3. publish the information matrix at the evaluation point (models.py:130):
-  // exact-phase passes, and the last iteration of the budget (a partition that
-  // stops in the approximate phase keeps its last Hessian); the copy of P^2
-  // values by one workgroup is skipped on the approximate iterations in between
+  // 3. publish the information matrix at the evaluation point (models.py:130)
+  // on exact-phase passes (the copy of P^2 values by one workgroup is skipped
+  // on the approximate iterations: a partition whose budget ends in the
+  // approximate phase gets its Sig_inv from the polish pass, eval_only, at
+  // the theta it returns)
   if (!a.subsample) {
-    if (phase == PHASE_F64 || a.last_iter) {
+    if (phase == PHASE_F64) {
       double* S = a.sig_inv + (int64_t)k * P * P;
       for (int e = tid; e < P * P; e += 1024) {
         const int i = e / P, j = e - i * P;
@@ -912,6 +918,7 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
     }
     if (tid == 0) a.loglik[k] = ll;
   }
+  if (a.eval_only) return;
   __syncthreads();
 
   // 4. blocked Cholesky H = L L^T, lower, in place -------------------------
@@ -1019,10 +1026,12 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
       return;
     }
     if (tid == 0) {
-      if (phase == PHASE_F32 && a.family == FAMILY_LOGISTIC) {
+      if (phase != PHASE_F64 && a.family == FAMILY_LOGISTIC) {
         // approximate Hessian lost definiteness: redo this point in fp64
         a.phase[k] = PHASE_F64;
         a.iters[k] = it + 1;
+        a.stall[k] = 0;
+        a.dm_prev[k] = 0.0;
         atomicAdd(&a.counters[PHASE_F64], 1);
       } else {
         a.status[k] = DLSA_STATUS_SINGULAR;
@@ -1157,8 +1166,14 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
     return;
   }
   int ph = phase;
-  if (ph == PHASE_F32) {
-    if (dm <= a.switch_tol * (1.0 + tm)) ph = PHASE_F64;
+  if (ph != PHASE_F64) {
+    if (dm <= a.switch_tol * (1.0 + tm)) {
+      ph = PHASE_F64;
+    } else {  // stall escalation (dlsa_internal.hpp): bf16 -> fp64 on this path
+      const double dprev = a.dm_prev[k];
+      ph = approx_stall_step(a, k, ph, dprev > 0.0 && dm > 0.5 * dprev);
+      if (ph == phase) a.dm_prev[k] = dm;
+    }
   } else if (dm <= a.tol * (1.0 + tm)) {
     a.status[k] = DLSA_STATUS_OK;
     a.phase[k] = PHASE_DONE;

@@ -63,8 +63,11 @@ def reduce_partitions_device(fit, n_rows=False):
     with ``n_rows`` one more entry holds the fitted row count, so the sharded
     path's single collective also carries N for the DBIC.
 
-    Partitions whose status is singular or nonfinite are summed as the
-    reference's all-zero frame (models.py:84-91) with a warning naming them:
+    Partitions that reached max_iter are summed as they are (last iterate,
+    Sig_inv = X^T W X at it: what the reference sums after sklearn's
+    ConvergenceWarning) with a warning.  Partitions whose status is singular
+    or nonfinite are summed as the reference's all-zero frame (models.py:84-91)
+    with a warning naming them:
     the reference's sklearn fit would not have produced a usable estimate
     either, and one NaN block would otherwise turn WLSE, ONESHOT and the
     LARS/DBIC path into NaN.  Empty / missing-level partitions already are
@@ -76,6 +79,13 @@ def reduce_partitions_device(fit, n_rows=False):
     P, K = fit.P, fit.K
     sig, sigt, th = fit.sig_inv, fit.sig_inv_theta, fit.theta
     st = fit.status.cpu().numpy()
+    slow = np.nonzero(st == 1)[0]
+    if slow.size:
+        # the reference sums whatever sklearn returns at max_iter (it only
+        # warns, ConvergenceWarning): such a partition is summed with its
+        # last iterate and the exact X^T W X at that iterate
+        warnings.warn("partitions " + str(slow.tolist()) + " reached max_iter before "
+                      "converging: summed with their last iterate and Sig_inv at it")
     bad = np.nonzero(np.isin(st, list(EXCLUDED_STATUS)))[0]
     if bad.size:
         warnings.warn("partitions " + str(bad.tolist()) + " ended "

@@ -126,8 +126,11 @@ def _batch_columns(chunk, ncols_hint=None):
     first = stripped[: stripped.find(b"\n")]
     n = first.count(b",") + 1 if ncols_hint is None else ncols_hint
     ro = pacsv.ReadOptions(column_names=[f"c{j}" for j in range(n)], block_size=1 << 26)
+    # empty lines are rows (the reference's split gives them one "" field):
+    # with more than one column pyarrow then rejects them as ragged, and the
+    # caller falls back to the reference's own loop
     po = pacsv.ParseOptions(delimiter=",", quote_char=False, escape_char=False,
-                            newlines_in_values=False)
+                            newlines_in_values=False, ignore_empty_lines=False)
     co = pacsv.ConvertOptions(column_types={f"c{j}": pa.string() for j in range(n)},
                               strings_can_be_null=False)
     return pacsv.read_csv(io.BytesIO(stripped), read_options=ro, parse_options=po,
@@ -141,8 +144,6 @@ def select_dummy_factors_from_file(file, header, dummy_columns, keep_top, replac
     are the raw text of the fields (strings), as the reference reads them."""
     import mmap
 
-    import pandas as pd
-
     path = os.path.expanduser(file)
     if os.path.getsize(path) == 0:
         return select_dummy_factors({}, keep_top, replace_with, pickle_file)
@@ -153,8 +154,32 @@ def select_dummy_factors_from_file(file, header, dummy_columns, keep_top, replac
         # non-ASCII text or "\r\n" line ends: the reference's own (slow) loop
         return _select_from_file_textmode(file, header, dummy_columns, keep_top, replace_with,
                                           pickle_file)
+    try:
+        dummy_dict = _counts_fast(data, header, dummy_columns)
+    except _Ragged:
+        # blank or whitespace-only lines, rows with a different field count:
+        # the reference pads short rows with None (pd.DataFrame of ragged
+        # lists) and counts a blank line as a row -- its own loop reproduces
+        # that exactly
+        return _select_from_file_textmode(file, header, dummy_columns, keep_top, replace_with,
+                                          pickle_file)
+    return select_dummy_factors(dummy_dict, keep_top, replace_with, pickle_file)
+
+
+class _Ragged(Exception):
+    pass
+
+
+def _counts_fast(data, header, dummy_columns):
+    """Level counts of every readlines buffer (pyarrow parse), merged in the
+    reference's order.  Raises _Ragged when a line's field count differs from
+    the file's first line (blank lines included)."""
+    import pandas as pd
+    import pyarrow as pa
+
     dummy_dict = {}
     names = None
+    ncols = None
     for bi, (a, b) in enumerate(readlines_batches(data)):
         chunk = data[a:b]
         if bi == 0 and header is True:
@@ -166,17 +191,24 @@ def select_dummy_factors_from_file(file, header, dummy_columns, keep_top, replac
             pdf = pd.DataFrame(columns=names if names is not None else [])
             counts = dummy_factors_counts(pdf, dummy_columns)
         else:
-            tab = _batch_columns(chunk)
+            try:
+                tab = _batch_columns(chunk, ncols)
+            except pa.ArrowInvalid as e:  # a row with another field count
+                raise _Ragged(str(e)) from e
+            ncols = tab.num_columns
+            if names is not None and ncols != len(names):
+                raise _Ragged("header and rows differ in field count")
             pdf = pd.DataFrame({(names[j] if names is not None else j): tab.column(j).to_numpy(
                 zero_copy_only=False).astype(object) for j in range(tab.num_columns)})
             counts = dummy_factors_counts(pdf, dummy_columns)
         dummy_dict = cumsum_dicts(dummy_dict, counts)
-    return select_dummy_factors(dummy_dict, keep_top, replace_with, pickle_file)
+    return dummy_dict
 
 
 def _select_from_file_textmode(file, header, dummy_columns, keep_top, replace_with, pickle_file):
     """Line-by-line restatement for files the fast path does not cover
-    (non-ASCII text, "\\r\\n" line ends): the reference's own loop."""
+    (non-ASCII text, "\\r\\n" line ends, blank lines, ragged rows): the
+    reference's own loop (dummies.py:111-146)."""
     import pandas as pd
 
     dummy_dict = {}

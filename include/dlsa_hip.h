@@ -51,7 +51,10 @@ extern "C" {
  * reference only warns (models.py:84-91,144-145); here every partition
  * reports what happened. */
 #define DLSA_STATUS_OK 0          /* converged */
-#define DLSA_STATUS_MAXITER 1     /* max_iter reached; last iterate returned */
+#define DLSA_STATUS_MAXITER 1     /* max_iter reached; the last iterate is returned
+                                     with Sig_inv = X^T W X evaluated at it (one
+                                     extra exact pass, as sklearn's model is used at
+                                     whatever coef it stopped at, models.py:114-130) */
 #define DLSA_STATUS_SINGULAR 2    /* X^T W X not positive definite */
 #define DLSA_STATUS_EMPTY 3       /* no rows: zero block, like models.py:84-91 */
 #define DLSA_STATUS_NONFINITE 4   /* NaN/Inf in the data or the iterates */
@@ -64,7 +67,10 @@ extern "C" {
  * approximate Hessians only steer Newton (the fp64 gradient fixes the
  * solution). */
 #define DLSA_HESSIAN_MIXED 0      /* bf16 MFMA Hessian until the step is below
-                                     switch_tol, then fp64 MFMA pass(es) */
+                                     switch_tol, then fp64 MFMA pass(es); a
+                                     partition whose step stops shrinking (two
+                                     iterations in a row without halving, or
+                                     backtracking) moves to fp32 MFMA, then fp64 */
 #define DLSA_HESSIAN_FP64 1       /* fp64 MFMA Hessian on every pass */
 #define DLSA_HESSIAN_MIXED_F32 2  /* as MIXED with fp32 MFMA approximate passes
                                      (for ill-conditioned designs) */
@@ -88,7 +94,10 @@ typedef struct dlsa_fit_options {
                                of the rows, never fewer than max(2048, 64 P))
                                to a 0.1-relative step, then on all rows to tol -- the
                                fixed point is unchanged; 0: all rows from the
-                               start */
+                               start.  Prefix iterations count against max_iter
+                               (a level takes at most half of what is left), so
+                               iters[k] <= max_iter and max_iter = 1 is one
+                               full-data Newton step from 0 */
   int32_t reserved[6];
 } dlsa_fit_options;
 
@@ -108,6 +117,10 @@ typedef struct dlsa_fit_stats {
                                ms_pass_fp32/fp64 hold the bf16 / fp64 Gram-pass time) */
   double ms_wide_gram;      /* P > DLSA_MAX_P_FUSED: Gram-pass kernel time */
   double ms_wide_assemble;  /* P > DLSA_MAX_P_FUSED: partial-tile assembly time */
+  int32_t passes_f32x;      /* of passes_fp32: fp32-MFMA passes of partitions that
+                               escalated from bf16 (stall / lost definiteness) */
+  int32_t polish_partitions; /* partitions left running by max_iter that got the
+                               exact pass publishing Sig_inv at their theta */
 } dlsa_fit_stats;
 
 /* Default options (mixed Hessian, automatic chunking, no timing). */

@@ -102,3 +102,42 @@ def test_readlines_batches_match_python(tmp_path):
                 ref.append((pos, pos + n))
                 pos += n
         assert readlines_batches(p.read_bytes()) == ref
+
+
+@pytest.mark.parametrize("kind", ["blank", "whitespace", "short", "long", "header_mismatch"])
+def test_file_selection_blank_and_ragged_lines_follow_reference_loop(tmp_path, kind):
+    """Inputs the pyarrow fast path cannot parse like the reference's
+    split-per-line loop (dummies.py:111-146): a blank line is a row whose
+    first field is "" (value_counts counts it), a short row is padded with
+    None (not counted), a long row widens the frame.  The product must give
+    the line loop's result (here: the module's own restatement of that loop,
+    which is the reference's code path step for step)."""
+    from dlsa_amd.dummies import _select_from_file_textmode, select_dummy_factors_from_file
+
+    rng = np.random.default_rng(7)
+    rows = [f"{rng.integers(0, 5)},{rng.choice(['a', 'b', 'c'])},{rng.random():.4f}"
+            for _ in range(3000)]
+    if kind == "blank":
+        rows[100] = ""
+        rows[2000] = ""
+    elif kind == "whitespace":
+        rows[50] = "   "
+    elif kind == "short":
+        rows[10] = "3,b"
+        rows[2500] = "1"
+    elif kind == "long":
+        rows[7] = "2,a,0.5,extra"
+    header = kind == "header_mismatch"
+    text = ("A,B\n" if header else "") + "\n".join(rows) + "\n"
+    path = tmp_path / "f.csv"
+    path.write_text(text)
+    cols = ["A", "B"] if header else [0, 1]
+    args = (str(path), header, cols, [0.9, 1.0], "000_OTHERS")
+    try:
+        want = _select_from_file_textmode(*args, None)
+    except Exception as e:  # the reference loop's own failure must be reproduced
+        with pytest.raises(type(e)):
+            select_dummy_factors_from_file(*args)
+        return
+    got = select_dummy_factors_from_file(*args)
+    assert _norm(got) == _norm(want)

@@ -375,3 +375,29 @@ def test_encode_categorical_unknown_rows():
     e = encode_categorical(df, "y", di, ["F_a"])
     assert e["unknown"] and e["unknown_rows"].tolist() == [False, False, True, False, False]
     assert e["codes"][:, 0].tolist() == [0, 1, 0, 2, 0]
+
+
+def test_bench_rejects_world_size_mismatch():
+    """bench.py refuses to run when the process group would not hold --gpus
+    ranks (before touching any GPU)."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert "WORLD_SIZE" in r.stderr
+
+
+def test_bench_host_cores_reports_quota():
+    import importlib.util
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    cores, info = b.host_cores()
+    assert 1 <= cores <= info["nproc"]
+    assert info["affinity"] <= info["nproc"]

@@ -69,3 +69,30 @@ def test_sharded_fit_two_ranks_one_gpu(golden_dir, shards):
         assert support == np.nonzero(gb)[0].tolist()
         ref = g["outs_noint"][shards[rank]][:, :, 1]
         assert np.abs(theta - ref).max() / np.abs(ref).max() < 1e-8
+
+
+def test_bench_gpus2_launches_two_ranks(tmp_path):
+    """`bench.py --gpus 2` started directly (no torchrun environment) must
+    spawn 2 ranks itself and report n_gpus = 2 with the sampled partitions at
+    parity; gloo lets both ranks share the one GPU of the test box (the
+    driver's multi-GPU run uses nccl = RCCL, one GPU per rank)."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--backend", "gloo",
+           "--n", "1600000", "--partitions", "16", "--steps", "2", "--warmup", "1",
+           "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2
+    assert out["scaling"] == "strong"
+    assert out["config"]["n_rows_job"] == 1600000 and out["config"]["partitions_job"] == 16
+    assert out["config"]["partitions_per_gpu"] == 8
+    assert out["parity_rel"] < 1e-8
