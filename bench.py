@@ -7,9 +7,10 @@
         --master-port P bench.py --gpus N --steps K --warmup W
 
 ``--gpus N`` with N > 1 and no torchrun environment starts the N ranks itself:
-the launcher process (which never touches the GPU) runs torch.distributed.run
-as a child process with the same arguments and exits with its code.  Every
-rank checks that the process group holds exactly N ranks.
+the launcher process (which never touches the GPU) starts N child processes
+of this script with the torch.distributed environment variables and exits
+with their status.  Every rank checks that the process group holds exactly N
+ranks.
 
 One step = one complete DLSA fit of the GPU's shard: batched Newton/IRLS over
 all partitions (approximate-Hessian passes + the final fp64 pass whose Hessian
@@ -532,10 +533,12 @@ def main():
 
 
 def launch_ranks(n):
-    """N ranks on this node without an external launcher: torch.distributed.run
-    as a CHILD process (this process never initialises the GPU, so no exec
-    from a GPU process), same arguments, rendezvous on 127.0.0.1 and a free
-    port.  Returns the child's exit code."""
+    """N ranks on this node without an external launcher: N child processes of
+    this script with the torch.distributed environment (RANK, LOCAL_RANK,
+    WORLD_SIZE, MASTER_ADDR = 127.0.0.1, a free MASTER_PORT) and the same
+    arguments.  This process never initialises the GPU (children, no exec).
+    If a rank fails the others are stopped (they would wait in a collective).
+    Returns the first non-zero exit code, else 0."""
     import socket
     import subprocess
 
@@ -543,10 +546,25 @@ def launch_ranks(n):
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-           f"--nproc-per-node={n}", "--master-addr=127.0.0.1", f"--master-port={port}",
-           os.path.abspath(__file__)] + sys.argv[1:]
-    return subprocess.call(cmd)
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in procs:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
 
 
 if __name__ == "__main__":

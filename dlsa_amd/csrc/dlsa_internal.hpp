@@ -99,10 +99,14 @@ struct SolveArgs {
 // wide_pass.hip).  With an approximate Hessian H~ and the exact gradient,
 // Newton contracts at rate ~ ||I - H~^-1 H|| (about kappa 2^-8 for bf16): on
 // an ill-conditioned design that rate nears 1 and the fit would crawl to
-// max_iter.  An approximate iteration "stalls" when its max |step| did not at
-// least halve against the previous one, or when it backtracks; two stalls in
-// a row move the partition one precision up (F32 -> escalate_to, F32X ->
-// F64).  Returns the phase to continue in.
+// max_iter.  Far from the MLE (Newton's damped phase) steps of similar size
+// are normal whatever the Hessian precision, so evidence is only taken once
+// the log-likelihood has gone quiet (the last step gained at most
+// kStallDll (1 + |ll|)): there an approximate iteration "stalls" when its max
+// |step| did not at least halve against the previous one, or when it
+// backtracks; two stalls in a row move the partition one precision up
+// (F32 -> escalate_to, F32X -> F64).  Returns the phase to continue in.
+constexpr double kStallDll = 1e-5;
 __device__ __forceinline__ int32_t escalate_phase(const SolveArgs& a, int32_t ph) {
   return ph == PHASE_F32 ? a.escalate_to : PHASE_F64;
 }
@@ -116,6 +120,24 @@ __device__ __forceinline__ int32_t approx_stall_step(const SolveArgs& a, int k, 
   }
   a.stall[k] = st;
   return ph;
+}
+// Approximate-phase iteration with a step of max |d| = dm (not yet below
+// switch_tol): log-likelihood ll at the pass's point, llp at the previous one.
+__device__ __forceinline__ int32_t approx_next_phase(const SolveArgs& a, int k, int32_t ph,
+                                                     double dm, double ll, double llp) {
+  if (!(ll - llp <= kStallDll * (1.0 + fabs(ll)))) {  // damped phase (or first iteration)
+    a.stall[k] = 0;
+    a.dm_prev[k] = 0.0;
+    return ph;
+  }
+  const double dp = a.dm_prev[k];
+  const int32_t nph = approx_stall_step(a, k, ph, dp > 0.0 && dm > 0.5 * dp);
+  if (nph == ph) a.dm_prev[k] = dm;
+  return nph;
+}
+// A backtracking approximate iteration: a stall only once the fit was quiet.
+__device__ __forceinline__ int32_t approx_backtrack_phase(const SolveArgs& a, int k, int32_t ph) {
+  return a.dm_prev[k] > 0.0 ? approx_stall_step(a, k, ph, true) : ph;
 }
 
 // Arguments of the log-likelihood evaluation pass.

@@ -197,8 +197,22 @@ constexpr int wave_rb(int NT, int W, int FAM) { return W * (64 / wave_lpr(NT, W,
 #ifndef DLSA_WAVE_OLS_NOMUL
 #define DLSA_WAVE_OLS_NOMUL 1
 #endif
+// Logistic: the row phase writes z = sqrt(w) x over x in the ring (and
+// sqrt(w) as the intercept operand), so the tile phase is pure MFMA with
+// A = B = z: H = Z^T Z.  On gfx950 an fp64 VALU op between fp64 MFMAs waits for
+// the MFMA pipe (no co-execution), so the w * x multiplies interleaved with
+// the MFMAs cost far more than their issue slots.
+#ifndef DLSA_WAVE_ZIMG
+#define DLSA_WAVE_ZIMG 0
+#endif
 #ifndef DLSA_WAVE_STRIP
 #define DLSA_WAVE_STRIP 1
+#endif
+// Profiling-only ablations (tools/build_variants.sh wab1 / wab2; product 0):
+// 1 = no row phase (w = 0.2 on the chunk's rows, no gradient / log-lik),
+// 2 = no tile phase (no operand reads, no MFMAs).
+#ifndef DLSA_WAVE_ABLATE
+#define DLSA_WAVE_ABLATE 0
 #endif
 constexpr int wave_strip_ns(int NT, int P) {
   return (!DLSA_WAVE_STRIP || NT < 2) ? 0
@@ -319,6 +333,8 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
   // OLS (w in {0, 1}): A operands are x itself (padded rows zeroed in the ring,
   // the intercept column = w)
   constexpr bool OLS_NOMUL = DLSA_WAVE_OLS_NOMUL && FAM == FAMILY_GAUSSIAN;
+  constexpr bool ZIMG = DLSA_WAVE_ZIMG && FAM == FAMILY_LOGISTIC;
+  constexpr bool NOMUL = OLS_NOMUL || ZIMG;  // tile phase without w * x
 
   const int lane = threadIdx.x & 63;
   const int p = a.p, P = a.P, ic = a.intercept;
@@ -374,7 +390,9 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
     const int rows_left = cx.nrows - b * RB;
 
     // ---- row phase: RW rows of this wave, LPR lanes per row -------------------
-    {
+    if constexpr (DLSA_WAVE_ABLATE == 1) {
+      if (sl == 0) wv[row] = row < rows_left ? 0.2 : 0.0;
+    } else {
       const bool valid = row < rows_left;
       double* xrw = xs + row * p + (sl - ic);
       double xv[M];
@@ -387,7 +405,7 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
           const int f = sl + LPR * m;
           // standardise in place for the tile phase (own row, own features;
           // the intercept slot f = 0 is the previous row's last value)
-          if (f >= ic && f < P) xrw[LPR * m] = v;
+          if (!ZIMG && f >= ic && f < P) xrw[LPR * m] = v;
         }
         if constexpr (OLS_NOMUL) {
           // OLS: w is 1 on rows of the chunk and 0 past it; zero the padded
@@ -424,12 +442,24 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
       }
 #pragma unroll
       for (int m = 0; m < M; ++m) gacc[m] = fma(xv[m], r, gacc[m]);
-      if (sl == 0) wv[row] = w;
+      if constexpr (ZIMG) {
+        // z = sqrt(w) x in place (own row, own features; padded rows: w = 0)
+        const double sw = sqrt(w);
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+          const int f = sl + LPR * m;
+          if (f >= ic && f < P) xrw[LPR * m] = xv[m] * sw;
+        }
+        if (sl == 0) wv[row] = sw;
+      } else {
+        if (sl == 0) wv[row] = w;
+      }
     }
     if constexpr (W > 1) wv_sync<W>();  // w (and standardised x) of all rows visible
 
     // ---- tile phase: KS k-steps of 4 rows, this wave's TW tiles ---------------
     // operands of k-step s+1 are read while the MFMAs of k-step s run
+    if constexpr (DLSA_WAVE_ABLATE == 2) continue;
     double xo[2][NC], xso[2][NSA], wk[2];
     auto load = [&](int s, int u) {
       const double* xq = xs + (4 * s + q) * p + (fl - ic);
@@ -452,14 +482,14 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         double v = xo[u][c];
-        if (c == 0 && icpt_lane) v = OLS_NOMUL ? wk[u] : 1.0;
+        if (c == 0 && icpt_lane) v = NOMUL ? wk[u] : 1.0;
         xv[c] = v;
-        if ((TL::RM >> c) & 1u) av[c] = OLS_NOMUL ? v : v * wk[u];
+        if ((TL::RM >> c) & 1u) av[c] = NOMUL ? v : v * wk[u];
       }
       double as[NSA];
       if constexpr (HAS_STRIP) {
 #pragma unroll
-        for (int r = 0; r < NS; ++r) as[r] = OLS_NOMUL ? xso[u][r] : xso[u][r] * wk[u];
+        for (int r = 0; r < NS; ++r) as[r] = NOMUL ? xso[u][r] : xso[u][r] * wk[u];
       }
       wv_static_for<TW>([&](auto iI) {
         constexpr int i = decltype(iI)::value;

@@ -159,7 +159,7 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
       a.iters[k] = it + 1;
       int ph = phase;
       if (!a.subsample && ph != PHASE_F64) {  // an approximate step that overshot
-        ph = approx_stall_step(a, k, ph, true);
+        ph = approx_backtrack_phase(a, k, ph);
         a.phase[k] = ph;
       }
       atomicAdd(&a.counters[ph], 1);
@@ -451,9 +451,7 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
       if (dm <= a.switch_tol * (1.0 + tm)) {
         ph = PHASE_F64;
       } else {
-        const double dp = a.dm_prev[k];
-        ph = approx_stall_step(a, k, ph, dp > 0.0 && dm > 0.5 * dp);
-        if (ph == phase) a.dm_prev[k] = dm;
+        ph = approx_next_phase(a, k, ph, dm, ll, llp);
       }
     } else if (dm <= a.tol * (1.0 + tm)) {
       a.status[k] = DLSA_STATUS_OK;

@@ -896,7 +896,7 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
       a.iters[k] = it + 1;
       int ph = phase;
       if (!a.subsample && ph != PHASE_F64) {  // an approximate step that overshot
-        ph = approx_stall_step(a, k, ph, true);
+        ph = approx_backtrack_phase(a, k, ph);
         a.phase[k] = ph;
       }
       atomicAdd(&a.counters[ph], 1);
@@ -1170,9 +1170,7 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
     if (dm <= a.switch_tol * (1.0 + tm)) {
       ph = PHASE_F64;
     } else {  // stall escalation (dlsa_internal.hpp): bf16 -> fp64 on this path
-      const double dprev = a.dm_prev[k];
-      ph = approx_stall_step(a, k, ph, dprev > 0.0 && dm > 0.5 * dprev);
-      if (ph == phase) a.dm_prev[k] = dm;
+      ph = approx_next_phase(a, k, ph, dm, ll, llp);
     }
   } else if (dm <= a.tol * (1.0 + tm)) {
     a.status[k] = DLSA_STATUS_OK;
