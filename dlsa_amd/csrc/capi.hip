@@ -118,9 +118,33 @@ static std::vector<double> warm_level_fracs(bool fused) {
 // and the full-data level always gets at least one; max_iter = 1 runs no
 // level at all.
 constexpr int kLevelIters = 10;
-static int iter_budget(bool final_level, int it, int max_iter) {
+static int iter_budget(bool final_level, int it, int max_iter, size_t lvl = 0) {
   if (final_level) return std::max(1, max_iter - it);
-  return std::min(kLevelIters, (max_iter - it) / 2);
+  int cap = kLevelIters;
+  // DLSA_LEVEL_MAXIT="a,b,...": iteration cap of warm-start level i (schedule
+  // experiments; a level may stop earlier at its step tolerance)
+  if (const char* e = getenv("DLSA_LEVEL_MAXIT")) {
+    const char* s = e;
+    for (size_t i = 0; *s; ++i) {
+      char* end = nullptr;
+      const long v = strtol(s, &end, 10);
+      if (end == s) break;
+      if (i == lvl && v > 0) cap = (int)v;
+      s = (*end == ',') ? end + 1 : end;
+    }
+  }
+  return std::min(cap, (max_iter - it) / 2);
+}
+
+// precision schedule knobs (SolveArgs::sched): DLSA_SCHED=1 enables it,
+// DLSA_SCHED_F32 / DLSA_SCHED_EXACT override its thresholds
+static void set_schedule(SolveArgs& sa) {
+  sa.sched = 0;
+  sa.sched_f32 = 1e-2;
+  sa.sched_exact = 3e-11;
+  if (const char* e = getenv("DLSA_SCHED")) sa.sched = atoi(e);
+  if (const char* e = getenv("DLSA_SCHED_F32")) sa.sched_f32 = atof(e);
+  if (const char* e = getenv("DLSA_SCHED_EXACT")) sa.sched_exact = atof(e);
 }
 // a level stops once its max relative step is below this; DLSA_LEVEL_TOL overrides
 // Pinned host staging of the per-iteration readbacks (running counters +
@@ -189,7 +213,7 @@ struct Layout {
   int64_t off_row0, off_rows, off_part, off_pcb, off_offsets;
   int64_t off_slabH, off_slabg, off_slabll;
   int64_t off_phase, off_bt, off_llprev, off_thprev, off_dprev, off_counters;
-  int64_t off_dmprev, off_stall;
+  int64_t off_dmprev, off_stall, off_stepprev;
   int64_t total;
 };
 
@@ -217,6 +241,7 @@ static Layout make_layout(const Plan& pl, int K) {
   L.off_counters = take(16);
   L.off_dmprev = take(8LL * K);
   L.off_stall = take(4LL * K);
+  L.off_stepprev = take(8LL * K);
   L.total = o;
   return L;
 }
@@ -259,7 +284,7 @@ struct WideLayout {
   int64_t off_g_row0, off_g_rows, off_g_part, off_gcb;
   int64_t off_offsets, off_w, off_slabg, off_slabll, off_slabG, off_slabgz, off_slabllz, off_H;
   int64_t off_phase, off_bt, off_llprev, off_thprev, off_dprev, off_counters;
-  int64_t off_dmprev, off_stall;
+  int64_t off_dmprev, off_stall, off_stepprev;
   int64_t total;
   int64_t cap_rows, cap_gram;  // row-chunk / Gram-row-group capacity of the tables and slabs
 };
@@ -309,6 +334,7 @@ static WideLayout make_wide_layout(const std::vector<WidePlans>& plans, int K, i
   L.off_counters = take(16);
   L.off_dmprev = take(8LL * K);
   L.off_stall = take(4LL * K);
+  L.off_stepprev = take(8LL * K);
   L.total = o;
   L.cap_rows = nr;
   L.cap_gram = ng;
@@ -606,6 +632,7 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
   sa.dm_prev = (double*)at(L.off_dmprev);
   sa.stall = (int32_t*)at(L.off_stall);
   sa.escalate_to = PHASE_F64;  // no fp32 fused wide pass: bf16 -> fp64
+  sa.step_prev = (double*)at(L.off_stepprev);
   sa.theta_prev = (double*)at(L.off_thprev);
   sa.delta_prev = (double*)at(L.off_dprev);
   sa.ll_prev = d_llprev;
@@ -656,10 +683,11 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
     sa.subsample = final_level ? 0 : 1;
     sa.level_tol = warm_level_tol(false);
     sa.switch_tol = final_level ? opt.switch_tol : 0.0;
-    const int it_end = it + iter_budget(final_level, it, max_iter);
+    const int it_end = it + iter_budget(final_level, it, max_iter, lvl);
     if (it_end <= it) continue;  // no budget left for this warm-start level
     DLSA_HIP_TRY(hipMemsetAsync(sa.dm_prev, 0, 8LL * K, stream));
     DLSA_HIP_TRY(hipMemsetAsync(sa.stall, 0, 4LL * K, stream));
+    DLSA_HIP_TRY(hipMemsetAsync(sa.step_prev, 0, 8LL * K, stream));
     for (; it < it_end && running_total(n_running) > 0 && q.rows.n_chunks > 0; ++it) {
       // approximate partitions: one fused pass (gradient + bf16 Hessian)
       if (n_running[PHASE_F32] > 0) {
@@ -918,6 +946,8 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
   sa.stall = (int32_t*)at(L.off_stall);
   // a stalled bf16-steered partition goes on with fp32-MFMA Hessians first
   sa.escalate_to = approx_prec == PREC_BF16 ? PHASE_F32X : PHASE_F64;
+  sa.step_prev = (double*)at(L.off_stepprev);
+  set_schedule(sa);
 
   const bool standardize = center != nullptr;
   StreamTimer timed{stream, opt.record_timing != 0};
@@ -976,10 +1006,11 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
     // a 0.2-relative step (warm_level_tol)
     sa.level_tol = warm_level_tol(true);
     sa.switch_tol = final_level ? opt.switch_tol : 0.0;
-    const int it_end = it + iter_budget(final_level, it, max_iter);
+    const int it_end = it + iter_budget(final_level, it, max_iter, lvl);
     if (it_end <= it) continue;  // no budget left for this warm-start level
     DLSA_HIP_TRY(hipMemsetAsync(sa.dm_prev, 0, 8LL * K, stream));
     DLSA_HIP_TRY(hipMemsetAsync(sa.stall, 0, 4LL * K, stream));
+    DLSA_HIP_TRY(hipMemsetAsync(sa.step_prev, 0, 8LL * K, stream));
     for (; it < it_end && running_total(n_running) > 0 && q.n_chunks > 0; ++it) {
       // approximate (bf16 or fp32), escalated fp32, then exact passes
       for (int ph : {PHASE_F32, PHASE_F32X, PHASE_F64}) {
@@ -1319,6 +1350,7 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
   sa.dm_prev = (double*)at(L.off_dmprev);
   sa.stall = (int32_t*)at(L.off_stall);
   sa.escalate_to = PHASE_F64;  // every categorical pass is exact
+  sa.step_prev = (double*)at(L.off_stepprev);
 
   const bool standardize = center != nullptr;
   StreamTimer timed{stream, opt.record_timing != 0};
@@ -1348,8 +1380,9 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
     sa.subsample = final_level ? 0 : 1;
     sa.level_tol = warm_level_tol(true);
     sa.switch_tol = 0.0;
-    const int it_end = it + iter_budget(final_level, it, max_iter);
+    const int it_end = it + iter_budget(final_level, it, max_iter, lvl);
     if (it_end <= it) continue;  // no budget left for this warm-start level
+    DLSA_HIP_TRY(hipMemsetAsync(sa.step_prev, 0, 8LL * K, stream));
     for (; it < it_end && n_running > 0 && qn.n_chunks > 0; ++it) {
       DLSA_HIP_TRY(timed(&g_stats.ms_pass_fp64,
                          [&] { return launch_cat_pass(ca, standardize, qn.n_chunks, stream); }));

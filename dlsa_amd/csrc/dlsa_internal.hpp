@@ -93,6 +93,14 @@ struct SolveArgs {
   double level_tol;   // warm-start level: stop when max|step| <= level_tol (1+max|theta|)
   int32_t escalate_to;  // next phase of a stalled PHASE_F32 partition (PHASE_F32X / PHASE_F64)
   int32_t eval_only;    // polish: publish Sig_inv / loglik at the current theta, no step
+  // precision schedule (sched = 1; see newton_solve.hip step 6): bf16 while
+  // the step exceeds sched_f32 (1 + max|theta|), then fp32 passes; the exact
+  // pass once the predicted error of the next iterate is below
+  // sched_exact (1 + max|theta|)
+  int32_t sched;
+  double sched_f32;
+  double sched_exact;
+  double* step_prev;  // [K] max |step| of the previous full-data iteration (0: none)
 };
 
 // Stall detection of the approximate phases (newton_solve.hip,

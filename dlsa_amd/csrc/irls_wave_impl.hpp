@@ -208,6 +208,20 @@ constexpr int wave_rb(int NT, int W, int FAM) { return W * (64 / wave_lpr(NT, W,
 #ifndef DLSA_WAVE_STRIP
 #define DLSA_WAVE_STRIP 1
 #endif
+// MF4 tile phase: every 16x16 tile as v_mfma_f64_4x4x4_4b sub-blocks.  On the
+// MI355X the 4x4x4_4b issues at ~75 TF/s against ~47 TF/s for 16x16x4
+// (tools/mfma4_probe.hip, profiles/r02_mfma4_probe.txt), and the exact pass
+// with 16x16x4 tiles runs at that 47 TF/s ceiling.  A 4x4x4_4b computes four
+// independent 4x4 blocks (block b: A lane i + 4b + 16k, B lane j + 4b + 16k,
+// D lane j + 4b + 16i), so with the 16x16x4 operands unchanged it yields the
+// diagonal 4x4 blocks (b, b) of a tile; A rotated by 4s lanes inside each
+// 16-lane row (DPP row_ror) yields blocks ((b - s) & 3, b).  A tile is 4
+// accumulators (s = 0..3), a diagonal tile 3 (s = 0, 2, 3: its lower blocks,
+// (3, 0) as the transpose of (0, 3)).  The rotations are per tile ROW (shared
+// by the row's tiles): 6 DPP moves per tile row and k-step.
+#ifndef DLSA_WAVE_MF4
+#define DLSA_WAVE_MF4 0
+#endif
 // Profiling-only ablations (tools/build_variants.sh wab1 / wab2; product 0):
 // 1 = no row phase (w = 0.2 on the chunk's rows, no gradient / log-lik),
 // 2 = no tile phase (no operand reads, no MFMAs).
@@ -222,9 +236,9 @@ constexpr int wave_strip_ns(int NT, int P) {
 }
 
 // MFMA time of tile row I in quarter tiles (a 4x4x4_4b ~ 1/4 of a 16x16x4
-// issue slot, conservatively)
+// issue slot, conservatively; MF4: a diagonal tile is 3 of them)
 constexpr int wave_row_cost(int NT, int NS, int I) {
-  return (NS > 0 && I == NT - 1) ? NT * NS : 4 * (I + 1);
+  return (NS > 0 && I == NT - 1) ? NT * NS : 4 * (I + 1) - (DLSA_WAVE_MF4 ? 1 : 0);
 }
 
 // tile rows of wave `wid`: rows are dealt most expensive first to the lighter
@@ -350,11 +364,18 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
 #pragma unroll
   for (int m = 0; m < M; ++m) gacc[m] = 0.0;
   double llacc = 0.0;
-  wd4 acc[TW];           // 16x16x4 tiles (AGPRs)
+  constexpr bool MF4 = DLSA_WAVE_MF4;
+  wd4 acc[MF4 ? 1 : TW];      // 16x16x4 tiles (AGPRs)
+  double macc[MF4 ? TW : 1][4];  // MF4: 4x4x4_4b accumulators of rotation s
   double sacc[TW][NSA];  // strip sub-blocks (the unused entries of either are dead)
 #pragma unroll
+  for (int i = 0; i < (MF4 ? 1 : TW); ++i) acc[i] = wd4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int i = 0; i < (MF4 ? TW : 1); ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) macc[i][r] = 0.0;
+#pragma unroll
   for (int i = 0; i < TW; ++i) {
-    acc[i] = wd4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int r = 0; r < NSA; ++r) sacc[i][r] = 0.0;
   }
@@ -491,26 +512,57 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
 #pragma unroll
         for (int r = 0; r < NS; ++r) as[r] = NOMUL ? xso[u][r] : xso[u][r] * wk[u];
       }
-      wv_static_for<TW>([&](auto iI) {
-        constexpr int i = decltype(iI)::value;
-        constexpr int I = TL::I_of(i), J = TL::J_of(i);
-        if constexpr (strip(I)) {
+      if constexpr (MF4) {
+        // A of each tile row rotated by 4 s lanes (s = 1..3) inside the 16-lane
+        // rows: block b of a 4x4x4_4b then pairs A group (b - s) & 3 with B group b
+        double ar[NT][4];
+        wv_static_for<NT>([&](auto iI) {
+          constexpr int I = decltype(iI)::value;
+          if constexpr (((TL::RM >> I) & 1u) && !strip(I)) {
+            ar[I][0] = av[I];
+            ar[I][1] = wv_dpp<0x124>(av[I]);  // row_ror:4
+            ar[I][2] = wv_dpp<0x128>(av[I]);  // row_ror:8
+            ar[I][3] = wv_dpp<0x12C>(av[I]);  // row_ror:12
+          }
+        });
+        wv_static_for<TW>([&](auto iI) {
+          constexpr int i = decltype(iI)::value;
+          constexpr int I = TL::I_of(i), J = TL::J_of(i);
+          if constexpr (strip(I)) {
 #pragma unroll
-          for (int r = 0; r < NS; ++r)
-            sacc[i][r] = __builtin_amdgcn_mfma_f64_4x4x4f64(as[r], xv[J], sacc[i][r], 0, 0, 0);
-        } else {
-          acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[I], xv[J], acc[i], 0, 0, 0);
-        }
-      });
+            for (int r = 0; r < NS; ++r)
+              sacc[i][r] = __builtin_amdgcn_mfma_f64_4x4x4f64(as[r], xv[J], sacc[i][r], 0, 0, 0);
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (I != J || r != 1)  // diagonal tile: s = 0, 2, 3
+                macc[i][r] = __builtin_amdgcn_mfma_f64_4x4x4f64(ar[I][r], xv[J], macc[i][r], 0, 0, 0);
+          }
+        });
+      } else {
+        wv_static_for<TW>([&](auto iI) {
+          constexpr int i = decltype(iI)::value;
+          constexpr int I = TL::I_of(i), J = TL::J_of(i);
+          if constexpr (strip(I)) {
+#pragma unroll
+            for (int r = 0; r < NS; ++r)
+              sacc[i][r] = __builtin_amdgcn_mfma_f64_4x4x4f64(as[r], xv[J], sacc[i][r], 0, 0, 0);
+          } else {
+            acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[I], xv[J], acc[i], 0, 0, 0);
+          }
+        });
+      }
     }
     // keep every 16x16x4 accumulator in AGPRs across the loop back edge (the
     // strip's 64-bit ones are left to the allocator: pinned one by one they
     // get shuffled between AGPRs; explicit capture: an asm operand alone does
     // not capture in a generic lambda)
-    wv_static_for<TW>([&acc](auto iI) {
-      constexpr int i = decltype(iI)::value;
-      if constexpr (!(NS > 0 && TL::I_of(i) == NT - 1)) asm volatile("" : "+a"(acc[i]));
-    });
+    if constexpr (!MF4) {
+      wv_static_for<TW>([&acc](auto iI) {
+        constexpr int i = decltype(iI)::value;
+        if constexpr (!(NS > 0 && TL::I_of(i) == NT - 1)) asm volatile("" : "+a"(acc[i]));
+      });
+    }
   }
   wv_wait_vmcnt<0>();
 
@@ -524,6 +576,21 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
       if constexpr (strip(TL::I_of(i))) {
         // sub-block r: rows 4 r + (l >> 4), columns l & 15; rows past it: 0
         sH[t * 256 + (4 * r + q) * 16 + fl] = r < NS ? sacc[i][r < NSA ? r : 0] : 0.0;
+      } else if constexpr (MF4) {
+        // rotation r: lane j + 4 b + 16 i holds H[4 ((b - r) & 3) + i][4 b + j]
+        const int bb = fl >> 2, row = 4 * ((bb - r) & 3) + q, col = fl;
+        if constexpr (TL::I_of(i) == TL::J_of(i)) {
+          // diagonal tile: its lower triangle only (the solve reads no more);
+          // block (0, 3) of rotation 3 is the transpose of the lower (3, 0)
+          if (r != 1) {
+            if (row >= col)
+              sH[t * 256 + row * 16 + col] = macc[i][r];
+            else if (r == 3 && bb == 3)
+              sH[t * 256 + col * 16 + row] = macc[i][r];
+          }
+        } else {
+          sH[t * 256 + row * 16 + col] = macc[i][r];
+        }
       } else {  // f64 16x16x4 C/D map: row = (l >> 4) + 4 r, col = l & 15
         sH[t * 256 + (q + 4 * r) * 16 + fl] = acc[i][r];
       }

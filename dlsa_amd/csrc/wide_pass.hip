@@ -179,6 +179,13 @@ __global__ __launch_bounds__(256) void wide_row_kernel(const WideArgs a) {
 // soffset (no address VALU); rows past the row group and columns >= p read 0
 // through the buffer range check.  Four k-steps of operands in flight.
 // ---------------------------------------------------------------------------
+// MF4 (as irls_wave_impl.hpp DLSA_WAVE_MF4): each 16x16 tile as four
+// v_mfma_f64_4x4x4_4b against the A operand rotated by 4 s lanes (DPP
+// row_ror), which issue at ~75 TF/s against ~47 TF/s for 16x16x4.
+#ifndef DLSA_GRAM_MF4
+#define DLSA_GRAM_MF4 0
+#endif
+
 template <bool STD>
 __global__ __launch_bounds__(256, 2) void wide_gram_kernel(const WideArgs a) {
   const int NB = a.NB;
@@ -232,7 +239,7 @@ __global__ __launch_bounds__(256, 2) void wide_gram_kernel(const WideArgs a) {
       wv_rsrc((uintptr_t)(a.X + row0 * p), (uintptr_t)nrows * (uintptr_t)p * 8u);
   const __amdgpu_buffer_rsrc_t wr = wv_rsrc((uintptr_t)(a.w + row0), (uintptr_t)nrows * 8u);
 
-  d4w acc[4][4];
+  d4w acc[4][4];  // 16x16x4: tile (s, u); MF4: rotation r of tile (s, u) in acc[s][u][r]
 #pragma unroll
   for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -266,11 +273,24 @@ __global__ __launch_bounds__(256, 2) void wide_gram_kernel(const WideArgs a) {
       av[s] = x * F.w;  // rows past the group: w = 0
       bv[s] = z;
     }
+#if DLSA_GRAM_MF4
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const double ar[4] = {av[s], wv_dpp<0x124>(av[s]), wv_dpp<0x128>(av[s]),
+                            wv_dpp<0x12C>(av[s])};
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          acc[s][u][r] = __builtin_amdgcn_mfma_f64_4x4x4f64(ar[r], bv[u], acc[s][u][r], 0, 0, 0);
+    }
+#else
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
       for (int u = 0; u < 4; ++u)
         acc[s][u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[u], acc[s][u], 0, 0, 0);
+#endif
   };
   const int nsteps = (nrows + 3) / 4;
   constexpr int DEPTH = 4;  // k-steps of operands in flight
@@ -291,7 +311,6 @@ __global__ __launch_bounds__(256, 2) void wide_gram_kernel(const WideArgs a) {
     }
   }
 
-  // C/D map of the f64 16x16x4 MFMA: row = (l >> 4) + 4 r, column = l & 15
   double* G = a.slab_G + ((int64_t)chunk * TB + t) * (GT * GT);
 #pragma unroll
   for (int s = 0; s < 4; ++s)
@@ -299,7 +318,13 @@ __global__ __launch_bounds__(256, 2) void wide_gram_kernel(const WideArgs a) {
     for (int u = 0; u < 4; ++u)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
+#if DLSA_GRAM_MF4
+        // rotation r: lane j + 4 b + 16 i holds tile element [4 ((b - r) & 3) + i][4 b + j]
+        const int i = 64 * qi + 16 * s + 4 * (((fl >> 2) - r) & 3) + kq;
+#else
+        // C/D map of the f64 16x16x4 MFMA: row = (l >> 4) + 4 r, column = l & 15
         const int i = 64 * qi + 16 * s + kq + 4 * r;
+#endif
         const int jc = 64 * qj + 16 * u + fl;
         G[i * GT + jc] = acc[s][u][r];
       }
@@ -1167,6 +1192,7 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
   }
   int ph = phase;
   if (ph != PHASE_F64) {
+    a.step_prev[k] = dm;
     if (dm <= a.switch_tol * (1.0 + tm)) {
       ph = PHASE_F64;
     } else {  // stall escalation (dlsa_internal.hpp): bf16 -> fp64 on this path

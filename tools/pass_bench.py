@@ -87,7 +87,7 @@ def main():
                     os.environ[k] = v
                 opt = _hip.FitOptions()
                 lib.dlsa_fit_options_default(ctypes.byref(opt))
-                opt.hessian_mode = 1 if args.hessian == "fp64" else 0
+                opt.hessian_mode = {"fp64": 1, "mixed_f32": 2}.get(args.hessian, 0)
                 opt.record_timing = 1
                 opt.rows_per_chunk = args.rows_per_chunk
                 opt.warm_start = args.warm
