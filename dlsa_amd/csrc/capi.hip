@@ -285,6 +285,7 @@ struct WideLayout {
   int64_t off_offsets, off_w, off_slabg, off_slabll, off_slabG, off_slabgz, off_slabllz, off_H;
   int64_t off_phase, off_bt, off_llprev, off_thprev, off_dprev, off_counters;
   int64_t off_dmprev, off_stall, off_stepprev;
+  int64_t off_sstate, off_sll, off_sg, off_sL;  // split Cholesky (wide_split_groups > 0)
   int64_t total;
   int64_t cap_rows, cap_gram;  // row-chunk / Gram-row-group capacity of the tables and slabs
 };
@@ -335,6 +336,11 @@ static WideLayout make_wide_layout(const std::vector<WidePlans>& plans, int K, i
   L.off_dmprev = take(8LL * K);
   L.off_stall = take(4LL * K);
   L.off_stepprev = take(8LL * K);
+  const bool split = wide_split_groups(K) > 0;
+  L.off_sstate = take(split ? 4LL * K : 0);
+  L.off_sll = take(split ? 8LL * K : 0);
+  L.off_sg = take(split ? 8LL * K * PP : 0);
+  L.off_sL = take(split ? 8LL * K * PP * PP : 0);
   L.total = o;
   L.cap_rows = nr;
   L.cap_gram = ng;
@@ -649,6 +655,9 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
   sa.switch_tol = opt.switch_tol;
 
   const bool standardize = center != nullptr;
+  WideSplitBuffers wsb{wide_split_groups(K), (int32_t*)at(L.off_sstate), (double*)at(L.off_sll),
+                       (double*)at(L.off_sg), (double*)at(L.off_sL)};
+  const WideSplitBuffers* split = wsb.groups > 0 ? &wsb : nullptr;
   StreamTimer timed{stream, opt.record_timing != 0};
   DLSA_HIP_TRY(timed.init());
   int32_t* h_cnt = pinned_staging(4 + (size_t)K);
@@ -711,8 +720,9 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
       DLSA_HIP_TRY(timed(&g_stats.ms_wide_assemble,
                          [&] { return launch_wide_assemble(wa, d_gcb, d_H, K, stream); }));
       DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
-      DLSA_HIP_TRY(timed(&g_stats.ms_solve,
-                         [&] { return launch_wide_newton(sa, wa, d_rcb, d_gcb, d_H, K, stream); }));
+      DLSA_HIP_TRY(timed(&g_stats.ms_solve, [&] {
+        return launch_wide_newton(sa, wa, d_rcb, d_gcb, d_H, K, stream, split);
+      }));
       DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, stream));
       DLSA_HIP_TRY(hipMemcpyAsync(h_phase, d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
       DLSA_HIP_TRY(hipStreamSynchronize(stream));

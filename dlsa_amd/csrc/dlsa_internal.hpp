@@ -258,8 +258,18 @@ hipError_t launch_wide_gram(const WideArgs& a, bool standardize, hipStream_t s);
 hipError_t launch_wide_fused(const WideArgs& a, bool standardize, hipStream_t s);
 hipError_t launch_wide_assemble(const WideArgs& a, const int32_t* gcb, double* Hfull, int K,
                                 hipStream_t s);
+// buffers of the split (multi-workgroup) wide Cholesky, wide_pass.hip
+struct WideSplitBuffers {
+  int groups;      // workgroups per partition in the panel kernels
+  int32_t* state;  // [K]
+  double* ll;      // [K]
+  double* g;       // [K, PP]
+  double* L;       // [K, PP, PP]
+};
+int wide_split_groups(int K);
 hipError_t launch_wide_newton(const SolveArgs& sa, const WideArgs& wa, const int32_t* rcb,
-                              const int32_t* gcb, double* Hfull, int K, hipStream_t s);
+                              const int32_t* gcb, double* Hfull, int K, hipStream_t s,
+                              const WideSplitBuffers* split = nullptr);
 int wide_newton_lds_bytes(int NB);
 hipError_t launch_loglik_eval(const EvalArgs& a, int n_chunks, hipStream_t s);
 hipError_t launch_loglik_reduce(const double* partial, const int32_t* pcb, int K, int B,

@@ -219,6 +219,10 @@ constexpr int wave_rb(int NT, int W, int FAM) { return W * (64 / wave_lpr(NT, W,
 // accumulators (s = 0..3), a diagonal tile 3 (s = 0, 2, 3: its lower blocks,
 // (3, 0) as the transpose of (0, 3)).  The rotations are per tile ROW (shared
 // by the row's tiles): 6 DPP moves per tile row and k-step.
+// DLSA_WAVE_MF4 = 1: every tile this way (measured slower: 26.4-26.8 vs
+// 25.2-25.4 ms per config-2 exact pass, profiles/r03c_mf4_sched_ab.txt);
+// 2: only the diagonal tiles (3 instead of 4 sub-block rotations, no upper
+// half), the others stay 16x16x4.
 #ifndef DLSA_WAVE_MF4
 #define DLSA_WAVE_MF4 0
 #endif
@@ -235,10 +239,15 @@ constexpr int wave_strip_ns(int NT, int P) {
                                       : 0;
 }
 
+// tile (I, J) as 4x4x4_4b rotations (MF4 = 1: every tile, 2: diagonal tiles)
+constexpr bool wave_use4(int I, int J) {
+  return DLSA_WAVE_MF4 == 1 || (DLSA_WAVE_MF4 == 2 && I == J);
+}
+
 // MFMA time of tile row I in quarter tiles (a 4x4x4_4b ~ 1/4 of a 16x16x4
 // issue slot, conservatively; MF4: a diagonal tile is 3 of them)
 constexpr int wave_row_cost(int NT, int NS, int I) {
-  return (NS > 0 && I == NT - 1) ? NT * NS : 4 * (I + 1) - (DLSA_WAVE_MF4 ? 1 : 0);
+  return (NS > 0 && I == NT - 1) ? NT * NS : 4 * (I + 1) - (DLSA_WAVE_MF4 == 1 ? 1 : DLSA_WAVE_MF4 == 2 ? 2 : 0);
 }
 
 // tile rows of wave `wid`: rows are dealt most expensive first to the lighter
@@ -364,12 +373,13 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
 #pragma unroll
   for (int m = 0; m < M; ++m) gacc[m] = 0.0;
   double llacc = 0.0;
-  constexpr bool MF4 = DLSA_WAVE_MF4;
-  wd4 acc[MF4 ? 1 : TW];      // 16x16x4 tiles (AGPRs)
+  constexpr bool MF4 = DLSA_WAVE_MF4 != 0;
+  constexpr bool ALL4 = DLSA_WAVE_MF4 == 1;
+  wd4 acc[ALL4 ? 1 : TW];      // 16x16x4 tiles (AGPRs)
   double macc[MF4 ? TW : 1][4];  // MF4: 4x4x4_4b accumulators of rotation s
   double sacc[TW][NSA];  // strip sub-blocks (the unused entries of either are dead)
 #pragma unroll
-  for (int i = 0; i < (MF4 ? 1 : TW); ++i) acc[i] = wd4{0.0, 0.0, 0.0, 0.0};
+  for (int i = 0; i < (ALL4 ? 1 : TW); ++i) acc[i] = wd4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
   for (int i = 0; i < (MF4 ? TW : 1); ++i)
 #pragma unroll
@@ -520,7 +530,7 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
           constexpr int I = decltype(iI)::value;
           if constexpr (((TL::RM >> I) & 1u) && !strip(I)) {
             ar[I][0] = av[I];
-            ar[I][1] = wv_dpp<0x124>(av[I]);  // row_ror:4
+            if constexpr (ALL4) ar[I][1] = wv_dpp<0x124>(av[I]);  // row_ror:4
             ar[I][2] = wv_dpp<0x128>(av[I]);  // row_ror:8
             ar[I][3] = wv_dpp<0x12C>(av[I]);  // row_ror:12
           }
@@ -532,11 +542,13 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
 #pragma unroll
             for (int r = 0; r < NS; ++r)
               sacc[i][r] = __builtin_amdgcn_mfma_f64_4x4x4f64(as[r], xv[J], sacc[i][r], 0, 0, 0);
-          } else {
+          } else if constexpr (wave_use4(I, J)) {
 #pragma unroll
             for (int r = 0; r < 4; ++r)
               if (I != J || r != 1)  // diagonal tile: s = 0, 2, 3
                 macc[i][r] = __builtin_amdgcn_mfma_f64_4x4x4f64(ar[I][r], xv[J], macc[i][r], 0, 0, 0);
+          } else {
+            acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[I], xv[J], acc[i], 0, 0, 0);
           }
         });
       } else {
@@ -557,10 +569,11 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
     // strip's 64-bit ones are left to the allocator: pinned one by one they
     // get shuffled between AGPRs; explicit capture: an asm operand alone does
     // not capture in a generic lambda)
-    if constexpr (!MF4) {
+    if constexpr (!ALL4) {
       wv_static_for<TW>([&acc](auto iI) {
         constexpr int i = decltype(iI)::value;
-        if constexpr (!(NS > 0 && TL::I_of(i) == NT - 1)) asm volatile("" : "+a"(acc[i]));
+        constexpr int I = TL::I_of(i), J = TL::J_of(i);
+        if constexpr (!(NS > 0 && I == NT - 1) && !wave_use4(I, J)) asm volatile("" : "+a"(acc[i]));
       });
     }
   }
@@ -576,7 +589,7 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
       if constexpr (strip(TL::I_of(i))) {
         // sub-block r: rows 4 r + (l >> 4), columns l & 15; rows past it: 0
         sH[t * 256 + (4 * r + q) * 16 + fl] = r < NS ? sacc[i][r < NSA ? r : 0] : 0.0;
-      } else if constexpr (MF4) {
+      } else if constexpr (wave_use4(TL::I_of(i), TL::J_of(i))) {
         // rotation r: lane j + 4 b + 16 i holds H[4 ((b - r) & 3) + i][4 b + j]
         const int bb = fl >> 2, row = 4 * ((bb - r) & 3) + q, col = fl;
         if constexpr (TL::I_of(i) == TL::J_of(i)) {

@@ -23,6 +23,7 @@ for v in "$@"; do
     wab2) D=DLSA_WAVE_ABLATE=2 ;;
     zimg) D=DLSA_WAVE_ZIMG=1 ;;
     mf4) D=DLSA_WAVE_MF4=1 ;;
+    mf4d) D=DLSA_WAVE_MF4=2 ;;
     gmf4) D=DLSA_GRAM_MF4=1 ;;
     nt) D=DLSA_X_DMA_AUX=2 ;;
     sc1) D=DLSA_X_DMA_AUX=1 ;;
