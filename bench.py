@@ -19,16 +19,17 @@ P^2+2P+2 sums (Sig_inv, Sig_inv theta, theta, K, N) across ranks, WLSE solve,
 LARS path and DBIC selection on the host.  Data are synthetic, generated in
 HBM by the counter-based generator before the timed region.
 
-Configs (BASELINE.json "configs"); sizes of the whole job under
---scaling strong (the default: rank r owns partitions [rK/N, (r+1)K/N) of the
-same global data set; config 2 is then north_star's "n=1e8,
-p=100, 1024 partitions on 8 GPUs"), or per GPU under --scaling weak (at N = 1
-the two are the same workload):
+Configs (BASELINE.json "configs").  Under --scaling strong (the
+default) n and K are those of the whole job and rank r owns partitions
+[rK/N, (r+1)K/N) of the same global data set (config 2 is then
+north_star's "n=1e8, p=100, 1024 partitions on 8 GPUs"); under --scaling weak
+they are per GPU.  Config 4's job (1e9 rows x 64 = 520 GB) does not fit one
+GPU, so it defaults to weak scaling with the 8-GPU job's per-GPU share:
   2  logistic n = 1e8, p = 100, K = 1024            (default; the headline metric)
-  3  logistic n = 1.5e7, p = 181 + intercept, K = 128 (airline-like dummy-coded design;
-                                                     1.2e8 rows on 8 GPUs)
+  3  logistic n = 1.2e8, p = 181 + intercept, K = 120 (airline-like dummy-coded design at
+                                                     the reference's 1e6 rows per partition)
   5  logistic n = 5e6, p = 500, K = 32              (wide path: row + Gram pass)
-  4  OLS      n = 1.25e8, p = 64, K = 128           (1e9 rows / 1024 partitions on 8 GPUs)
+  4  OLS      n = 1.25e8, p = 64, K = 128 per GPU   (1e9 rows / 1024 partitions on 8 GPUs)
 
 Rank 0 prints one JSON line (metric/value/... plus "roofline" for the dominant
 kernel, "parity_rel" of two sampled partitions against the CPU oracle after
@@ -54,12 +55,12 @@ FP64_MFMA_PEAK_TF = 78.6   # MI355X fp64 matrix (spec; = fp64 vector on CDNA4)
 CONFIGS = {
     2: dict(n=100_000_000, p=100, K=1024, family="logistic",
             name="config2: synthetic logistic n=1e8, p=100, K=1024 partitions"),
-    3: dict(n=15_000_000, p=181, K=128, family="logistic", data="dummy", intercept=True,
-            name="config3: airline-like logistic n=1.5e7 (1.2e8 on 8 GPUs), 9 numeric + "
-                 "172 dummy columns + intercept, K=128 partitions"),
+    3: dict(n=120_000_000, p=181, K=120, family="logistic", data="dummy", intercept=True,
+            name="config3: airline-like logistic n=1.2e8, 9 numeric + 172 dummy columns + "
+                 "intercept, K=120 partitions (1e6 rows each, logistic_dlsa.py:239-240)"),
     5: dict(n=5_000_000, p=500, K=32, family="logistic",
             name="config5: synthetic logistic n=5e6, p=500, K=32 partitions (wide path)"),
-    4: dict(n=125_000_000, p=64, K=128, family="ols",
+    4: dict(n=125_000_000, p=64, K=128, family="ols", scaling="weak",
             name="config4: synthetic OLS n=1.25e8 (1e9 on 8 GPUs), p=64, K=128 partitions"),
 }
 
@@ -198,9 +199,9 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
-    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
-                    help="strong (default): n and K of the whole job, partitions sharded over "
-                         "the ranks; weak: the config's n and K per GPU")
+    ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
+                    help="strong (default; config 4: weak): n and K of the whole job, "
+                         "partitions sharded over the ranks; weak: the config's n and K per GPU")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group transport for N > 1 (nccl = RCCL over xGMI; gloo: "
                          "host transport, lets several ranks share one GPU in tests)")
@@ -221,6 +222,8 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))
     cfg = dict(CONFIGS[args.config])
+    if args.scaling is None:
+        args.scaling = cfg.get("scaling", "strong")
     for key, v in (("n", args.n), ("p", args.p), ("K", args.partitions)):
         if v:
             cfg[key] = v
@@ -510,7 +513,7 @@ def main():
     }
     if rank == 0 and not args.no_parity:
         # checker, after the timed region: the last step's fit of this rank
-        sample = [0] if wide else None
+        sample = [0] if (wide or data == "dummy") else None  # 1e6-row / P = 500 oracles
         rel, smp = sampled_parity(fit, X, y, offsets, family, codes=codes, levels=levels,
                                   fit_intercept=fit_intercept, sample=sample)
         out["parity_rel"] = rel
@@ -521,7 +524,7 @@ def main():
         if args.config == 5:
             nk_cpu, parts = 20000, 16      # ~8 s of single-thread work per partition
         else:                              # ~10-30 s of single-thread work in all
-            nk_cpu, parts = n // K, {2: 32, 3: 32, 4: 128}[args.config]
+            nk_cpu, parts = min(n // K, 125_000), {2: 32, 3: 32, 4: 128}[args.config]
         parts = args.cpu_parts or max(parts, 2 * workers)  # >= 2 partitions per core
         out["cpu_baseline"] = cpu_baseline(nk_cpu, p, parts, workers, family, data=data)
         out["cpu_baseline"].update(cinfo)

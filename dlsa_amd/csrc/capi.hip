@@ -118,33 +118,9 @@ static std::vector<double> warm_level_fracs(bool fused) {
 // and the full-data level always gets at least one; max_iter = 1 runs no
 // level at all.
 constexpr int kLevelIters = 10;
-static int iter_budget(bool final_level, int it, int max_iter, size_t lvl = 0) {
+static int iter_budget(bool final_level, int it, int max_iter) {
   if (final_level) return std::max(1, max_iter - it);
-  int cap = kLevelIters;
-  // DLSA_LEVEL_MAXIT="a,b,...": iteration cap of warm-start level i (schedule
-  // experiments; a level may stop earlier at its step tolerance)
-  if (const char* e = getenv("DLSA_LEVEL_MAXIT")) {
-    const char* s = e;
-    for (size_t i = 0; *s; ++i) {
-      char* end = nullptr;
-      const long v = strtol(s, &end, 10);
-      if (end == s) break;
-      if (i == lvl && v > 0) cap = (int)v;
-      s = (*end == ',') ? end + 1 : end;
-    }
-  }
-  return std::min(cap, (max_iter - it) / 2);
-}
-
-// precision schedule knobs (SolveArgs::sched): DLSA_SCHED=1 enables it,
-// DLSA_SCHED_F32 / DLSA_SCHED_EXACT override its thresholds
-static void set_schedule(SolveArgs& sa) {
-  sa.sched = 0;
-  sa.sched_f32 = 1e-2;
-  sa.sched_exact = 3e-11;
-  if (const char* e = getenv("DLSA_SCHED")) sa.sched = atoi(e);
-  if (const char* e = getenv("DLSA_SCHED_F32")) sa.sched_f32 = atof(e);
-  if (const char* e = getenv("DLSA_SCHED_EXACT")) sa.sched_exact = atof(e);
+  return std::min(kLevelIters, (max_iter - it) / 2);
 }
 // a level stops once its max relative step is below this; DLSA_LEVEL_TOL overrides
 // Pinned host staging of the per-iteration readbacks (running counters +
@@ -213,7 +189,7 @@ struct Layout {
   int64_t off_row0, off_rows, off_part, off_pcb, off_offsets;
   int64_t off_slabH, off_slabg, off_slabll;
   int64_t off_phase, off_bt, off_llprev, off_thprev, off_dprev, off_counters;
-  int64_t off_dmprev, off_stall, off_stepprev;
+  int64_t off_dmprev, off_stall;
   int64_t total;
 };
 
@@ -241,7 +217,6 @@ static Layout make_layout(const Plan& pl, int K) {
   L.off_counters = take(16);
   L.off_dmprev = take(8LL * K);
   L.off_stall = take(4LL * K);
-  L.off_stepprev = take(8LL * K);
   L.total = o;
   return L;
 }
@@ -284,8 +259,7 @@ struct WideLayout {
   int64_t off_g_row0, off_g_rows, off_g_part, off_gcb;
   int64_t off_offsets, off_w, off_slabg, off_slabll, off_slabG, off_slabgz, off_slabllz, off_H;
   int64_t off_phase, off_bt, off_llprev, off_thprev, off_dprev, off_counters;
-  int64_t off_dmprev, off_stall, off_stepprev;
-  int64_t off_sstate, off_sll, off_sg, off_sL;  // split Cholesky (wide_split_groups > 0)
+  int64_t off_dmprev, off_stall;
   int64_t total;
   int64_t cap_rows, cap_gram;  // row-chunk / Gram-row-group capacity of the tables and slabs
 };
@@ -335,12 +309,6 @@ static WideLayout make_wide_layout(const std::vector<WidePlans>& plans, int K, i
   L.off_counters = take(16);
   L.off_dmprev = take(8LL * K);
   L.off_stall = take(4LL * K);
-  L.off_stepprev = take(8LL * K);
-  const bool split = wide_split_groups(K) > 0;
-  L.off_sstate = take(split ? 4LL * K : 0);
-  L.off_sll = take(split ? 8LL * K : 0);
-  L.off_sg = take(split ? 8LL * K * PP : 0);
-  L.off_sL = take(split ? 8LL * K * PP * PP : 0);
   L.total = o;
   L.cap_rows = nr;
   L.cap_gram = ng;
@@ -638,7 +606,6 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
   sa.dm_prev = (double*)at(L.off_dmprev);
   sa.stall = (int32_t*)at(L.off_stall);
   sa.escalate_to = PHASE_F64;  // no fp32 fused wide pass: bf16 -> fp64
-  sa.step_prev = (double*)at(L.off_stepprev);
   sa.theta_prev = (double*)at(L.off_thprev);
   sa.delta_prev = (double*)at(L.off_dprev);
   sa.ll_prev = d_llprev;
@@ -655,9 +622,6 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
   sa.switch_tol = opt.switch_tol;
 
   const bool standardize = center != nullptr;
-  WideSplitBuffers wsb{wide_split_groups(K), (int32_t*)at(L.off_sstate), (double*)at(L.off_sll),
-                       (double*)at(L.off_sg), (double*)at(L.off_sL)};
-  const WideSplitBuffers* split = wsb.groups > 0 ? &wsb : nullptr;
   StreamTimer timed{stream, opt.record_timing != 0};
   DLSA_HIP_TRY(timed.init());
   int32_t* h_cnt = pinned_staging(4 + (size_t)K);
@@ -692,11 +656,10 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
     sa.subsample = final_level ? 0 : 1;
     sa.level_tol = warm_level_tol(false);
     sa.switch_tol = final_level ? opt.switch_tol : 0.0;
-    const int it_end = it + iter_budget(final_level, it, max_iter, lvl);
+    const int it_end = it + iter_budget(final_level, it, max_iter);
     if (it_end <= it) continue;  // no budget left for this warm-start level
     DLSA_HIP_TRY(hipMemsetAsync(sa.dm_prev, 0, 8LL * K, stream));
     DLSA_HIP_TRY(hipMemsetAsync(sa.stall, 0, 4LL * K, stream));
-    DLSA_HIP_TRY(hipMemsetAsync(sa.step_prev, 0, 8LL * K, stream));
     for (; it < it_end && running_total(n_running) > 0 && q.rows.n_chunks > 0; ++it) {
       // approximate partitions: one fused pass (gradient + bf16 Hessian)
       if (n_running[PHASE_F32] > 0) {
@@ -720,9 +683,8 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
       DLSA_HIP_TRY(timed(&g_stats.ms_wide_assemble,
                          [&] { return launch_wide_assemble(wa, d_gcb, d_H, K, stream); }));
       DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
-      DLSA_HIP_TRY(timed(&g_stats.ms_solve, [&] {
-        return launch_wide_newton(sa, wa, d_rcb, d_gcb, d_H, K, stream, split);
-      }));
+      DLSA_HIP_TRY(timed(&g_stats.ms_solve,
+                         [&] { return launch_wide_newton(sa, wa, d_rcb, d_gcb, d_H, K, stream); }));
       DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, stream));
       DLSA_HIP_TRY(hipMemcpyAsync(h_phase, d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
       DLSA_HIP_TRY(hipStreamSynchronize(stream));
@@ -956,8 +918,6 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
   sa.stall = (int32_t*)at(L.off_stall);
   // a stalled bf16-steered partition goes on with fp32-MFMA Hessians first
   sa.escalate_to = approx_prec == PREC_BF16 ? PHASE_F32X : PHASE_F64;
-  sa.step_prev = (double*)at(L.off_stepprev);
-  set_schedule(sa);
 
   const bool standardize = center != nullptr;
   StreamTimer timed{stream, opt.record_timing != 0};
@@ -1016,11 +976,10 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
     // a 0.2-relative step (warm_level_tol)
     sa.level_tol = warm_level_tol(true);
     sa.switch_tol = final_level ? opt.switch_tol : 0.0;
-    const int it_end = it + iter_budget(final_level, it, max_iter, lvl);
+    const int it_end = it + iter_budget(final_level, it, max_iter);
     if (it_end <= it) continue;  // no budget left for this warm-start level
     DLSA_HIP_TRY(hipMemsetAsync(sa.dm_prev, 0, 8LL * K, stream));
     DLSA_HIP_TRY(hipMemsetAsync(sa.stall, 0, 4LL * K, stream));
-    DLSA_HIP_TRY(hipMemsetAsync(sa.step_prev, 0, 8LL * K, stream));
     for (; it < it_end && running_total(n_running) > 0 && q.n_chunks > 0; ++it) {
       // approximate (bf16 or fp32), escalated fp32, then exact passes
       for (int ph : {PHASE_F32, PHASE_F32X, PHASE_F64}) {
@@ -1304,13 +1263,15 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
   DLSA_HIP_TRY(hipMemcpyAsync(h_phase.data(), d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
   DLSA_HIP_TRY(hipStreamSynchronize(stream));
   {
-    // fixed-point grids: 2^E with |term| * 2^E * (rows of a chunk) <= 2^61
-    int64_t rmax = 1;
+    // fixed-point grids: 2^E with |term| * 2^E * max(rows of a chunk, 1024) <= 2^60,
+    // so a bin's sum stays in int64 and every term below 2^50 (the kernel's
+    // 1.5 * 2^52 rounding needs |term| < 2^51)
+    int64_t rmax = 1024;
     for (const Plan& qn : plans)
       for (int c = 0; c < qn.n_chunks; ++c) rmax = std::max<int64_t>(rmax, qn.chunk_rows[c]);
     auto grid = [&](double bound) {  // bound: max |term|
       if (!(bound > 0) || !std::isfinite(bound)) bound = 1.0;
-      const int e = (int)std::floor(61.0 - std::log2(bound * (double)rmax));
+      const int e = (int)std::floor(60.0 - std::log2(bound * (double)rmax));
       return std::ldexp(1.0, std::max(-900, std::min(900, e)));
     };
     ca.hscale[0] = grid(0.25);  // w = mu (1 - mu) <= 1/4; pair cells
@@ -1360,7 +1321,6 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
   sa.dm_prev = (double*)at(L.off_dmprev);
   sa.stall = (int32_t*)at(L.off_stall);
   sa.escalate_to = PHASE_F64;  // every categorical pass is exact
-  sa.step_prev = (double*)at(L.off_stepprev);
 
   const bool standardize = center != nullptr;
   StreamTimer timed{stream, opt.record_timing != 0};
@@ -1390,9 +1350,8 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
     sa.subsample = final_level ? 0 : 1;
     sa.level_tol = warm_level_tol(true);
     sa.switch_tol = 0.0;
-    const int it_end = it + iter_budget(final_level, it, max_iter, lvl);
+    const int it_end = it + iter_budget(final_level, it, max_iter);
     if (it_end <= it) continue;  // no budget left for this warm-start level
-    DLSA_HIP_TRY(hipMemsetAsync(sa.step_prev, 0, 8LL * K, stream));
     for (; it < it_end && n_running > 0 && qn.n_chunks > 0; ++it) {
       DLSA_HIP_TRY(timed(&g_stats.ms_pass_fp64,
                          [&] { return launch_cat_pass(ca, standardize, qn.n_chunks, stream); }));

@@ -48,10 +48,18 @@
 
 namespace dlsa {
 
-// fixed-point term: v * scale rounded to an integer (two's complement add)
+// fixed-point term: v * scale rounded to the nearest integer, added as a
+// two's-complement int64.  The rounding is the 1.5 * 2^52 trick: for
+// |x| < 2^51, x + 1.5 * 2^52 has ulp 1, so one FMA rounds v * scale (exactly,
+// once) and the low bits of the sum minus those of 1.5 * 2^52 are the
+// integer -- an FMA and a 64-bit integer subtraction instead of the emulated
+// f64 -> i64 conversion (7 VALU ops, 5 of them fp64).  The grids (capi.hip
+// fit_categorical) bound every term by 2^50.
 __device__ __forceinline__ void lds_add(unsigned long long* p, double v, double scale) {
-  const unsigned long long t = (unsigned long long)__double2ll_rn(v * scale);
-  __hip_atomic_fetch_add(p, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  const double t = fma(v, scale, 6755399441055744.0);  // 1.5 * 2^52
+  const unsigned long long u =
+      (unsigned long long)__double_as_longlong(t) - 0x4338000000000000ull;
+  __hip_atomic_fetch_add(p, u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ long long hist_at(const unsigned long long* h, int i) {
   return (long long)h[i];
@@ -111,6 +119,11 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
 
   const int64_t row0 = a.chunk_row0[chunk];
   const int nrows = a.chunk_rows[chunk];
+  // fixed-point scales in registers (not re-read from the kernel arguments
+  // inside the row loop): [0] w, [1] residual, [2 + i - ic] w x_i
+  double hsc[QN + 2];
+#pragma unroll
+  for (int i = 0; i < QN + 2; ++i) hsc[i] = (i < 2 + q && i < kCatQMax + 2) ? a.hscale[i] : 0.0;
   double hacc[NTRI], gacc[QN], llacc = 0.0;
 #pragma unroll
   for (int i = 0; i < NTRI; ++i) hacc[i] = 0.0;
@@ -176,12 +189,16 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
         const int slot = (lane & t_ndrep[f]) * t_nlev[f] + cv[f] - 1;
         unsigned long long* h = hist + t_ndoff[f] + slot * a.nd_stride;
         if constexpr (!(DLSA_CAT_ABLATE & 1)) {
-          lds_add(h, w, a.hscale[0]);
+          lds_add(h, w, hsc[0]);
 #pragma unroll
-          for (int i = 0; i < QN; ++i)  // numeric columns (register index compile-time)
-            if (i >= ic && i < Qn) lds_add(h + 1 + (i - ic), w * xv[i], a.hscale[2 + i - ic]);
+          for (int i = 0; i < QN; ++i) {  // numeric columns (register index compile-time)
+            // parameter i is numeric column i - ic: scale hsc[2 + i - ic]
+            // (both candidate indices compile-time: no dynamic register index)
+            const double sc = ic ? hsc[i + 1] : hsc[i + 2];
+            if (i >= ic && i < Qn) lds_add(h + 1 + (i - ic), w * xv[i], sc);
+          }
         }
-        if constexpr (!(DLSA_CAT_ABLATE & 4)) lds_add(hist + t_goff[f] + slot, res, a.hscale[1]);
+        if constexpr (!(DLSA_CAT_ABLATE & 4)) lds_add(hist + t_goff[f] + slot, res, hsc[1]);
       }
     }
 #pragma unroll
@@ -192,7 +209,7 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
           const int pi = cat_pair(f, g, F);
           const int rep = lane & t_prrep[pi];
           lds_add(hist + t_proff[pi] + (rep * t_nlev[f] + cv[f] - 1) * t_nlev[g] + cv[g] - 1, w,
-                  a.hscale[0]);
+                  hsc[0]);
         }
       }
   }

@@ -93,14 +93,6 @@ struct SolveArgs {
   double level_tol;   // warm-start level: stop when max|step| <= level_tol (1+max|theta|)
   int32_t escalate_to;  // next phase of a stalled PHASE_F32 partition (PHASE_F32X / PHASE_F64)
   int32_t eval_only;    // polish: publish Sig_inv / loglik at the current theta, no step
-  // precision schedule (sched = 1; see newton_solve.hip step 6): bf16 while
-  // the step exceeds sched_f32 (1 + max|theta|), then fp32 passes; the exact
-  // pass once the predicted error of the next iterate is below
-  // sched_exact (1 + max|theta|)
-  int32_t sched;
-  double sched_f32;
-  double sched_exact;
-  double* step_prev;  // [K] max |step| of the previous full-data iteration (0: none)
 };
 
 // Stall detection of the approximate phases (newton_solve.hip,
@@ -258,18 +250,8 @@ hipError_t launch_wide_gram(const WideArgs& a, bool standardize, hipStream_t s);
 hipError_t launch_wide_fused(const WideArgs& a, bool standardize, hipStream_t s);
 hipError_t launch_wide_assemble(const WideArgs& a, const int32_t* gcb, double* Hfull, int K,
                                 hipStream_t s);
-// buffers of the split (multi-workgroup) wide Cholesky, wide_pass.hip
-struct WideSplitBuffers {
-  int groups;      // workgroups per partition in the panel kernels
-  int32_t* state;  // [K]
-  double* ll;      // [K]
-  double* g;       // [K, PP]
-  double* L;       // [K, PP, PP]
-};
-int wide_split_groups(int K);
 hipError_t launch_wide_newton(const SolveArgs& sa, const WideArgs& wa, const int32_t* rcb,
-                              const int32_t* gcb, double* Hfull, int K, hipStream_t s,
-                              const WideSplitBuffers* split = nullptr);
+                              const int32_t* gcb, double* Hfull, int K, hipStream_t s);
 int wide_newton_lds_bytes(int NB);
 hipError_t launch_loglik_eval(const EvalArgs& a, int n_chunks, hipStream_t s);
 hipError_t launch_loglik_reduce(const double* partial, const int32_t* pcb, int K, int B,

@@ -197,40 +197,8 @@ constexpr int wave_rb(int NT, int W, int FAM) { return W * (64 / wave_lpr(NT, W,
 #ifndef DLSA_WAVE_OLS_NOMUL
 #define DLSA_WAVE_OLS_NOMUL 1
 #endif
-// Logistic: the row phase writes z = sqrt(w) x over x in the ring (and
-// sqrt(w) as the intercept operand), so the tile phase is pure MFMA with
-// A = B = z: H = Z^T Z.  On gfx950 an fp64 VALU op between fp64 MFMAs waits for
-// the MFMA pipe (no co-execution), so the w * x multiplies interleaved with
-// the MFMAs cost far more than their issue slots.
-#ifndef DLSA_WAVE_ZIMG
-#define DLSA_WAVE_ZIMG 0
-#endif
 #ifndef DLSA_WAVE_STRIP
 #define DLSA_WAVE_STRIP 1
-#endif
-// MF4 tile phase: every 16x16 tile as v_mfma_f64_4x4x4_4b sub-blocks.  On the
-// MI355X the 4x4x4_4b issues at ~75 TF/s against ~47 TF/s for 16x16x4
-// (tools/mfma4_probe.hip, profiles/r02_mfma4_probe.txt), and the exact pass
-// with 16x16x4 tiles runs at that 47 TF/s ceiling.  A 4x4x4_4b computes four
-// independent 4x4 blocks (block b: A lane i + 4b + 16k, B lane j + 4b + 16k,
-// D lane j + 4b + 16i), so with the 16x16x4 operands unchanged it yields the
-// diagonal 4x4 blocks (b, b) of a tile; A rotated by 4s lanes inside each
-// 16-lane row (DPP row_ror) yields blocks ((b - s) & 3, b).  A tile is 4
-// accumulators (s = 0..3), a diagonal tile 3 (s = 0, 2, 3: its lower blocks,
-// (3, 0) as the transpose of (0, 3)).  The rotations are per tile ROW (shared
-// by the row's tiles): 6 DPP moves per tile row and k-step.
-// DLSA_WAVE_MF4 = 1: every tile this way (measured slower: 26.4-26.8 vs
-// 25.2-25.4 ms per config-2 exact pass, profiles/r03c_mf4_sched_ab.txt);
-// 2: only the diagonal tiles (3 instead of 4 sub-block rotations, no upper
-// half), the others stay 16x16x4.
-#ifndef DLSA_WAVE_MF4
-#define DLSA_WAVE_MF4 0
-#endif
-// Profiling-only ablations (tools/build_variants.sh wab1 / wab2; product 0):
-// 1 = no row phase (w = 0.2 on the chunk's rows, no gradient / log-lik),
-// 2 = no tile phase (no operand reads, no MFMAs).
-#ifndef DLSA_WAVE_ABLATE
-#define DLSA_WAVE_ABLATE 0
 #endif
 constexpr int wave_strip_ns(int NT, int P) {
   return (!DLSA_WAVE_STRIP || NT < 2) ? 0
@@ -239,15 +207,10 @@ constexpr int wave_strip_ns(int NT, int P) {
                                       : 0;
 }
 
-// tile (I, J) as 4x4x4_4b rotations (MF4 = 1: every tile, 2: diagonal tiles)
-constexpr bool wave_use4(int I, int J) {
-  return DLSA_WAVE_MF4 == 1 || (DLSA_WAVE_MF4 == 2 && I == J);
-}
-
 // MFMA time of tile row I in quarter tiles (a 4x4x4_4b ~ 1/4 of a 16x16x4
-// issue slot, conservatively; MF4: a diagonal tile is 3 of them)
+// issue slot, conservatively)
 constexpr int wave_row_cost(int NT, int NS, int I) {
-  return (NS > 0 && I == NT - 1) ? NT * NS : 4 * (I + 1) - (DLSA_WAVE_MF4 == 1 ? 1 : DLSA_WAVE_MF4 == 2 ? 2 : 0);
+  return (NS > 0 && I == NT - 1) ? NT * NS : 4 * (I + 1);
 }
 
 // tile rows of wave `wid`: rows are dealt most expensive first to the lighter
@@ -356,8 +319,6 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
   // OLS (w in {0, 1}): A operands are x itself (padded rows zeroed in the ring,
   // the intercept column = w)
   constexpr bool OLS_NOMUL = DLSA_WAVE_OLS_NOMUL && FAM == FAMILY_GAUSSIAN;
-  constexpr bool ZIMG = DLSA_WAVE_ZIMG && FAM == FAMILY_LOGISTIC;
-  constexpr bool NOMUL = OLS_NOMUL || ZIMG;  // tile phase without w * x
 
   const int lane = threadIdx.x & 63;
   const int p = a.p, P = a.P, ic = a.intercept;
@@ -373,19 +334,11 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
 #pragma unroll
   for (int m = 0; m < M; ++m) gacc[m] = 0.0;
   double llacc = 0.0;
-  constexpr bool MF4 = DLSA_WAVE_MF4 != 0;
-  constexpr bool ALL4 = DLSA_WAVE_MF4 == 1;
-  wd4 acc[ALL4 ? 1 : TW];      // 16x16x4 tiles (AGPRs)
-  double macc[MF4 ? TW : 1][4];  // MF4: 4x4x4_4b accumulators of rotation s
+  wd4 acc[TW];           // 16x16x4 tiles (AGPRs)
   double sacc[TW][NSA];  // strip sub-blocks (the unused entries of either are dead)
 #pragma unroll
-  for (int i = 0; i < (ALL4 ? 1 : TW); ++i) acc[i] = wd4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int i = 0; i < (MF4 ? TW : 1); ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) macc[i][r] = 0.0;
-#pragma unroll
   for (int i = 0; i < TW; ++i) {
+    acc[i] = wd4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int r = 0; r < NSA; ++r) sacc[i][r] = 0.0;
   }
@@ -421,9 +374,7 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
     const int rows_left = cx.nrows - b * RB;
 
     // ---- row phase: RW rows of this wave, LPR lanes per row -------------------
-    if constexpr (DLSA_WAVE_ABLATE == 1) {
-      if (sl == 0) wv[row] = row < rows_left ? 0.2 : 0.0;
-    } else {
+    {
       const bool valid = row < rows_left;
       double* xrw = xs + row * p + (sl - ic);
       double xv[M];
@@ -436,7 +387,7 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
           const int f = sl + LPR * m;
           // standardise in place for the tile phase (own row, own features;
           // the intercept slot f = 0 is the previous row's last value)
-          if (!ZIMG && f >= ic && f < P) xrw[LPR * m] = v;
+          if (f >= ic && f < P) xrw[LPR * m] = v;
         }
         if constexpr (OLS_NOMUL) {
           // OLS: w is 1 on rows of the chunk and 0 past it; zero the padded
@@ -473,24 +424,12 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
       }
 #pragma unroll
       for (int m = 0; m < M; ++m) gacc[m] = fma(xv[m], r, gacc[m]);
-      if constexpr (ZIMG) {
-        // z = sqrt(w) x in place (own row, own features; padded rows: w = 0)
-        const double sw = sqrt(w);
-#pragma unroll
-        for (int m = 0; m < M; ++m) {
-          const int f = sl + LPR * m;
-          if (f >= ic && f < P) xrw[LPR * m] = xv[m] * sw;
-        }
-        if (sl == 0) wv[row] = sw;
-      } else {
-        if (sl == 0) wv[row] = w;
-      }
+      if (sl == 0) wv[row] = w;
     }
     if constexpr (W > 1) wv_sync<W>();  // w (and standardised x) of all rows visible
 
     // ---- tile phase: KS k-steps of 4 rows, this wave's TW tiles ---------------
     // operands of k-step s+1 are read while the MFMAs of k-step s run
-    if constexpr (DLSA_WAVE_ABLATE == 2) continue;
     double xo[2][NC], xso[2][NSA], wk[2];
     auto load = [&](int s, int u) {
       const double* xq = xs + (4 * s + q) * p + (fl - ic);
@@ -513,69 +452,35 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         double v = xo[u][c];
-        if (c == 0 && icpt_lane) v = NOMUL ? wk[u] : 1.0;
+        if (c == 0 && icpt_lane) v = OLS_NOMUL ? wk[u] : 1.0;
         xv[c] = v;
-        if ((TL::RM >> c) & 1u) av[c] = NOMUL ? v : v * wk[u];
+        if ((TL::RM >> c) & 1u) av[c] = OLS_NOMUL ? v : v * wk[u];
       }
       double as[NSA];
       if constexpr (HAS_STRIP) {
 #pragma unroll
-        for (int r = 0; r < NS; ++r) as[r] = NOMUL ? xso[u][r] : xso[u][r] * wk[u];
+        for (int r = 0; r < NS; ++r) as[r] = OLS_NOMUL ? xso[u][r] : xso[u][r] * wk[u];
       }
-      if constexpr (MF4) {
-        // A of each tile row rotated by 4 s lanes (s = 1..3) inside the 16-lane
-        // rows: block b of a 4x4x4_4b then pairs A group (b - s) & 3 with B group b
-        double ar[NT][4];
-        wv_static_for<NT>([&](auto iI) {
-          constexpr int I = decltype(iI)::value;
-          if constexpr (((TL::RM >> I) & 1u) && !strip(I)) {
-            ar[I][0] = av[I];
-            if constexpr (ALL4) ar[I][1] = wv_dpp<0x124>(av[I]);  // row_ror:4
-            ar[I][2] = wv_dpp<0x128>(av[I]);  // row_ror:8
-            ar[I][3] = wv_dpp<0x12C>(av[I]);  // row_ror:12
-          }
-        });
-        wv_static_for<TW>([&](auto iI) {
-          constexpr int i = decltype(iI)::value;
-          constexpr int I = TL::I_of(i), J = TL::J_of(i);
-          if constexpr (strip(I)) {
+      wv_static_for<TW>([&](auto iI) {
+        constexpr int i = decltype(iI)::value;
+        constexpr int I = TL::I_of(i), J = TL::J_of(i);
+        if constexpr (strip(I)) {
 #pragma unroll
-            for (int r = 0; r < NS; ++r)
-              sacc[i][r] = __builtin_amdgcn_mfma_f64_4x4x4f64(as[r], xv[J], sacc[i][r], 0, 0, 0);
-          } else if constexpr (wave_use4(I, J)) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              if (I != J || r != 1)  // diagonal tile: s = 0, 2, 3
-                macc[i][r] = __builtin_amdgcn_mfma_f64_4x4x4f64(ar[I][r], xv[J], macc[i][r], 0, 0, 0);
-          } else {
-            acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[I], xv[J], acc[i], 0, 0, 0);
-          }
-        });
-      } else {
-        wv_static_for<TW>([&](auto iI) {
-          constexpr int i = decltype(iI)::value;
-          constexpr int I = TL::I_of(i), J = TL::J_of(i);
-          if constexpr (strip(I)) {
-#pragma unroll
-            for (int r = 0; r < NS; ++r)
-              sacc[i][r] = __builtin_amdgcn_mfma_f64_4x4x4f64(as[r], xv[J], sacc[i][r], 0, 0, 0);
-          } else {
-            acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[I], xv[J], acc[i], 0, 0, 0);
-          }
-        });
-      }
+          for (int r = 0; r < NS; ++r)
+            sacc[i][r] = __builtin_amdgcn_mfma_f64_4x4x4f64(as[r], xv[J], sacc[i][r], 0, 0, 0);
+        } else {
+          acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[I], xv[J], acc[i], 0, 0, 0);
+        }
+      });
     }
     // keep every 16x16x4 accumulator in AGPRs across the loop back edge (the
     // strip's 64-bit ones are left to the allocator: pinned one by one they
     // get shuffled between AGPRs; explicit capture: an asm operand alone does
     // not capture in a generic lambda)
-    if constexpr (!ALL4) {
-      wv_static_for<TW>([&acc](auto iI) {
-        constexpr int i = decltype(iI)::value;
-        constexpr int I = TL::I_of(i), J = TL::J_of(i);
-        if constexpr (!(NS > 0 && I == NT - 1) && !wave_use4(I, J)) asm volatile("" : "+a"(acc[i]));
-      });
-    }
+    wv_static_for<TW>([&acc](auto iI) {
+      constexpr int i = decltype(iI)::value;
+      if constexpr (!(NS > 0 && TL::I_of(i) == NT - 1)) asm volatile("" : "+a"(acc[i]));
+    });
   }
   wv_wait_vmcnt<0>();
 
@@ -589,21 +494,6 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
       if constexpr (strip(TL::I_of(i))) {
         // sub-block r: rows 4 r + (l >> 4), columns l & 15; rows past it: 0
         sH[t * 256 + (4 * r + q) * 16 + fl] = r < NS ? sacc[i][r < NSA ? r : 0] : 0.0;
-      } else if constexpr (wave_use4(TL::I_of(i), TL::J_of(i))) {
-        // rotation r: lane j + 4 b + 16 i holds H[4 ((b - r) & 3) + i][4 b + j]
-        const int bb = fl >> 2, row = 4 * ((bb - r) & 3) + q, col = fl;
-        if constexpr (TL::I_of(i) == TL::J_of(i)) {
-          // diagonal tile: its lower triangle only (the solve reads no more);
-          // block (0, 3) of rotation 3 is the transpose of the lower (3, 0)
-          if (r != 1) {
-            if (row >= col)
-              sH[t * 256 + row * 16 + col] = macc[i][r];
-            else if (r == 3 && bb == 3)
-              sH[t * 256 + col * 16 + row] = macc[i][r];
-          }
-        } else {
-          sH[t * 256 + row * 16 + col] = macc[i][r];
-        }
       } else {  // f64 16x16x4 C/D map: row = (l >> 4) + 4 r, col = l & 15
         sH[t * 256 + (q + 4 * r) * 16 + fl] = acc[i][r];
       }

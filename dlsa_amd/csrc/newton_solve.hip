@@ -448,27 +448,10 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
       return;
     }
     if (ph != PHASE_F64) {
-      const double sp = a.step_prev[k];
-      a.step_prev[k] = dm;
       if (dm <= a.switch_tol * (1.0 + tm)) {
         ph = PHASE_F64;
       } else {
         ph = approx_next_phase(a, k, ph, dm, ll, llp);
-        if (a.sched && ph == phase) {
-          // error of the next iterate ~ the step it will take: Newton contracts
-          // quadratically once the Hessian is close, d_{k+1} ~ d_k (d_k /
-          // d_{k-1})^2; an fp32-Hessian iteration adds ~1e-7 d_k at most, a
-          // bf16 one ~1e-3 d_k (its own linear rate), so the exact pass is
-          // entered only after an fp32 iteration
-          const double r = sp > 0.0 ? fmin(1.0, dm / sp) : 1.0;
-          const double en = dm * r * r;
-          if (ph == PHASE_F32X && en <= a.sched_exact * (1.0 + tm)) {
-            ph = PHASE_F64;
-          } else if (ph == PHASE_F32 && a.escalate_to == PHASE_F32X &&
-                     dm <= a.sched_f32 * (1.0 + tm)) {
-            ph = PHASE_F32X;
-          }
-        }
       }
     } else if (dm <= a.tol * (1.0 + tm)) {
       a.status[k] = DLSA_STATUS_OK;

@@ -179,13 +179,6 @@ __global__ __launch_bounds__(256) void wide_row_kernel(const WideArgs a) {
 // soffset (no address VALU); rows past the row group and columns >= p read 0
 // through the buffer range check.  Four k-steps of operands in flight.
 // ---------------------------------------------------------------------------
-// MF4 (as irls_wave_impl.hpp DLSA_WAVE_MF4): each 16x16 tile as four
-// v_mfma_f64_4x4x4_4b against the A operand rotated by 4 s lanes (DPP
-// row_ror), which issue at ~75 TF/s against ~47 TF/s for 16x16x4.
-#ifndef DLSA_GRAM_MF4
-#define DLSA_GRAM_MF4 0
-#endif
-
 template <bool STD>
 __global__ __launch_bounds__(256, 2) void wide_gram_kernel(const WideArgs a) {
   const int NB = a.NB;
@@ -239,7 +232,7 @@ __global__ __launch_bounds__(256, 2) void wide_gram_kernel(const WideArgs a) {
       wv_rsrc((uintptr_t)(a.X + row0 * p), (uintptr_t)nrows * (uintptr_t)p * 8u);
   const __amdgpu_buffer_rsrc_t wr = wv_rsrc((uintptr_t)(a.w + row0), (uintptr_t)nrows * 8u);
 
-  d4w acc[4][4];  // 16x16x4: tile (s, u); MF4: rotation r of tile (s, u) in acc[s][u][r]
+  d4w acc[4][4];
 #pragma unroll
   for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -273,24 +266,11 @@ __global__ __launch_bounds__(256, 2) void wide_gram_kernel(const WideArgs a) {
       av[s] = x * F.w;  // rows past the group: w = 0
       bv[s] = z;
     }
-#if DLSA_GRAM_MF4
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const double ar[4] = {av[s], wv_dpp<0x124>(av[s]), wv_dpp<0x128>(av[s]),
-                            wv_dpp<0x12C>(av[s])};
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          acc[s][u][r] = __builtin_amdgcn_mfma_f64_4x4x4f64(ar[r], bv[u], acc[s][u][r], 0, 0, 0);
-    }
-#else
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
       for (int u = 0; u < 4; ++u)
         acc[s][u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[u], acc[s][u], 0, 0, 0);
-#endif
   };
   const int nsteps = (nrows + 3) / 4;
   constexpr int DEPTH = 4;  // k-steps of operands in flight
@@ -311,6 +291,7 @@ __global__ __launch_bounds__(256, 2) void wide_gram_kernel(const WideArgs a) {
     }
   }
 
+  // C/D map of the f64 16x16x4 MFMA: row = (l >> 4) + 4 r, column = l & 15
   double* G = a.slab_G + ((int64_t)chunk * TB + t) * (GT * GT);
 #pragma unroll
   for (int s = 0; s < 4; ++s)
@@ -318,13 +299,7 @@ __global__ __launch_bounds__(256, 2) void wide_gram_kernel(const WideArgs a) {
     for (int u = 0; u < 4; ++u)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-#if DLSA_GRAM_MF4
-        // rotation r: lane j + 4 b + 16 i holds tile element [4 ((b - r) & 3) + i][4 b + j]
-        const int i = 64 * qi + 16 * s + 4 * (((fl >> 2) - r) & 3) + kq;
-#else
-        // C/D map of the f64 16x16x4 MFMA: row = (l >> 4) + 4 r, column = l & 15
         const int i = 64 * qi + 16 * s + kq + 4 * r;
-#endif
         const int jc = 64 * qj + 16 * u + fl;
         G[i * GT + jc] = acc[s][u][r];
       }
@@ -850,41 +825,16 @@ __global__ __launch_bounds__(256) void wide_assemble_kernel(const WideArgs a, co
 }
 
 // ---------------------------------------------------------------------------
-// per-partition Newton update.  MODE_ALL: one 1024-thread workgroup per
-// partition does everything (step control, blocked Cholesky in place in H,
-// solves, update).  Split form (DLSA_WIDE_SPLIT): MODE_PRE does the step
-// control and publishes (steps 1-3), wide_chol_panel_kernel factors one
-// 32-column panel per launch with G workgroups per partition (the trailing
-// update spread over G CUs instead of one: K = 32 partitions fill 32 of 256
-// CUs otherwise), writing L to its own buffer, and MODE_POST does the solves
-// and the update (steps 5-6).
+// per-partition Newton update (one 1024-thread workgroup per partition)
 // ---------------------------------------------------------------------------
-enum : int { WN_ALL = 0, WN_PRE = 1, WN_POST = 2 };
-// split-state of a partition between the kernels: 0 nothing to factor,
-// 1 factorization running / done, 2 not positive definite
-struct WideSplit {
-  int32_t* state;  // [K]
-  double* ll;      // [K] log-likelihood of the pass
-  double* g;       // [K, PP] gradient of the pass
-  double* L;       // [K, PP, PP] Cholesky factor (lower)
-};
-
-template <int MODE>
 __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, const WideArgs wa,
                                                            const int32_t* rcb, const int32_t* gcb,
-                                                           double* Hfull, const WideSplit sp) {
+                                                           double* Hfull) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int k = blockIdx.x;
+  if (a.status[k] != STATUS_RUNNING) return;
+  if (a.phase[k] != PHASE_F32 && a.phase[k] != PHASE_F64) return;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  if constexpr (MODE == WN_PRE) {
-    if (tid == 0) sp.state[k] = 0;
-  }
-  if constexpr (MODE == WN_POST) {
-    if (sp.state[k] == 0) return;  // block-uniform
-  } else {
-    if (a.status[k] != STATUS_RUNNING) return;
-    if (a.phase[k] != PHASE_F32 && a.phase[k] != PHASE_F64) return;
-  }
   const int P = a.P, PP = GT * wa.NB;
   double* L11 = sm;             // [CB][LDP] diagonal block
   double* Lp = L11 + CB * LDP;  // [PP][LDP] panel below it (scratch in the solves)
@@ -893,16 +843,6 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
   double* red = z + PP;         // [64]: [0..47] reductions, [40] ll, [48] flag
   int* flag = (int*)(red + 48);
   double* H = Hfull + (int64_t)k * PP * PP;
-  // the factor the solves read: H itself (MODE_ALL) or the split form's L
-  const double* Lf = MODE == WN_POST ? sp.L + (int64_t)k * PP * PP : H;
-  if constexpr (MODE == WN_POST) {
-    for (int f = tid; f < PP; f += 1024) g[f] = sp.g[(int64_t)k * PP + f];
-    if (tid == 0) {
-      red[40] = sp.ll[k];
-      *flag = sp.state[k] == 2 ? 1 : 0;
-    }
-    __syncthreads();
-  } else {
 
   // 1. gradient and log-likelihood of the pass, in chunk order: the fused
   // pass's row groups (PHASE_F32) or the row pass's chunks (PHASE_F64)
@@ -923,7 +863,6 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
   }
   if (tid == 0) *flag = 0;
   __syncthreads();
-  }
   const double ll = red[40];
   const int it = a.iters[k];
   const int phase = a.phase[k];
@@ -936,8 +875,6 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
       a.iters[k] = it + 1;
     }
   };
-  const double llp = a.ll_prev[k];
-  if constexpr (MODE != WN_POST) {
   if (!isfinite(ll)) {
     if (a.subsample)
       level_fail();
@@ -946,6 +883,7 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
     return;
   }
   // 2. step halving on a log-likelihood decrease (newton_solve.hip step 2)
+  const double llp = a.ll_prev[k];
   if (!a.eval_only && a.family == FAMILY_LOGISTIC && it > 0 &&
       ll < llp - 1e-6 * (1.0 + fabs(llp)) && a.backtracks[k] < 40) {
     const int bt = a.backtracks[k] + 1;
@@ -981,20 +919,11 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
     if (tid == 0) a.loglik[k] = ll;
   }
   if (a.eval_only) return;
-  if constexpr (MODE == WN_PRE) {  // hand over to the panel kernels
-    for (int f = tid; f < PP; f += 1024) sp.g[(int64_t)k * PP + f] = g[f];
-    if (tid == 0) {
-      sp.ll[k] = ll;
-      sp.state[k] = 1;
-    }
-    return;
-  }
   __syncthreads();
-  }  // MODE != WN_POST
 
   // 4. blocked Cholesky H = L L^T, lower, in place -------------------------
   const int fl = lane & 15, kq = lane >> 4;
-  for (int jb = 0; jb < PP && MODE == WN_ALL; jb += CB) {
+  for (int jb = 0; jb < PP; jb += CB) {
     {  // diagonal block -> LDS (one element per thread)
       const int i = tid >> 5, c = tid & 31;
       L11[i * LDP + c] = c <= i ? H[(int64_t)(jb + i) * PP + jb + c] : 0.0;
@@ -1117,7 +1046,7 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
   for (int jb = 0; jb < PP; jb += CB) {
     if (wid == 0) {  // diagonal block by one wave: lane i = row i
       const int i = lane & 31;
-      const double* hr = Lf + (int64_t)(jb + i) * PP + jb;
+      const double* hr = H + (int64_t)(jb + i) * PP + jb;
       double lrow[CB];
 #pragma unroll
       for (int c = 0; c < CB; ++c) lrow[c] = c <= i ? hr[c] : 0.0;
@@ -1134,7 +1063,7 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
     const int rest = PP - jb - CB;
     if (tid < rest) {  // rows below: z_i -= L[i][jb:jb+32] z[jb:jb+32]
       const int i = jb + CB + tid;
-      const double* hr = Lf + (int64_t)i * PP + jb;
+      const double* hr = H + (int64_t)i * PP + jb;
       double s = z[i];
 #pragma unroll
       for (int c = 0; c < CB; ++c) s -= hr[c] * z[jb + c];
@@ -1147,7 +1076,7 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
     {  // u_c = sum_{i >= jb + CB} L[i][jb + c] d_i, thread (c, row group)
       const int c = tid & 31, grp = tid >> 5;
       double s = 0.0;
-      for (int i = jb + CB + grp; i < PP; i += 32) s += Lf[(int64_t)i * PP + jb + c] * z[i];
+      for (int i = jb + CB + grp; i < PP; i += 32) s += H[(int64_t)i * PP + jb + c] * z[i];
       Lp[grp * LDP + c] = s;
     }
     __syncthreads();
@@ -1159,7 +1088,7 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
       double v = z[jb + c] - u;
       double lcol[CB];  // column c of L11: L[r][c], r >= c
 #pragma unroll
-      for (int r = 0; r < CB; ++r) lcol[r] = r >= c ? Lf[(int64_t)(jb + r) * PP + jb + c] : 0.0;
+      for (int r = 0; r < CB; ++r) lcol[r] = r >= c ? H[(int64_t)(jb + r) * PP + jb + c] : 0.0;
 #pragma unroll
       for (int r = CB - 1; r >= 0; --r) {
         if (c == r) v = v / lcol[r];
@@ -1238,7 +1167,6 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
   }
   int ph = phase;
   if (ph != PHASE_F64) {
-    a.step_prev[k] = dm;
     if (dm <= a.switch_tol * (1.0 + tm)) {
       ph = PHASE_F64;
     } else {  // stall escalation (dlsa_internal.hpp): bf16 -> fp64 on this path
@@ -1251,123 +1179,6 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
   }
   a.phase[k] = ph;
   atomicAdd(&a.counters[ph], 1);
-}
-
-// One 32-column panel jb of the split Cholesky, grid (G, K) x 1024 threads.
-// Every workgroup of a partition factors the diagonal block and solves the
-// panel below it (L21 = A21 L11^-T) -- redundant, cheap, and no workgroup
-// depends on another's writes inside a launch; workgroup 0 writes L11 and L21
-// to the factor buffer.  The trailing lower tiles A22 -= L21 L21^T (16x16,
-// fp64 MFMA) are dealt to the G workgroups, each tile read and written by
-// exactly one of them; nothing this launch writes in H is read in it.
-__global__ __launch_bounds__(1024) void wide_chol_panel_kernel(const WideArgs wa, double* Hfull,
-                                                               const WideSplit sp, int jb) {
-  extern __shared__ __attribute__((aligned(16))) double sm[];
-  const int g = blockIdx.x, G = gridDim.x, k = blockIdx.y;
-  if (sp.state[k] != 1) return;  // block-uniform
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int PP = GT * wa.NB;
-  double* L11 = sm;             // [CB][LDP]
-  double* Lp = L11 + CB * LDP;  // [PP][LDP]
-  int* flag = (int*)(Lp + PP * LDP);
-  double* H = Hfull + (int64_t)k * PP * PP;
-  double* Lf = sp.L + (int64_t)k * PP * PP;
-  if (tid == 0) *flag = 0;
-  {  // diagonal block -> LDS (one element per thread)
-    const int i = tid >> 5, c = tid & 31;
-    L11[i * LDP + c] = c <= i ? H[(int64_t)(jb + i) * PP + jb + c] : 0.0;
-  }
-  __syncthreads();
-  if (wid == 0) {  // unblocked factor, lane i holds row i (as wide_newton_kernel)
-    const int i = lane & 31;
-    double row[CB];
-#pragma unroll
-    for (int c = 0; c < CB; ++c) row[c] = L11[i * LDP + c];
-    bool ok = true;
-#pragma unroll
-    for (int j = 0; j < CB; ++j) {
-      const double d = bcast_f64(row[j], j);
-      ok = ok && d > 0.0 && isfinite(d);
-      const double ljj = sqrt(d);
-      if (i == j) row[j] = ljj;
-      if (i > j) row[j] = row[j] / ljj;
-#pragma unroll
-      for (int c = j + 1; c < CB; ++c) {
-        const double lcj = bcast_f64(row[j], c);
-        if (i >= c) row[c] -= row[j] * lcj;
-      }
-    }
-    if (lane < 32) {
-#pragma unroll
-      for (int c = 0; c < CB; ++c) {
-        const double v = c <= i ? row[c] : 0.0;
-        L11[i * LDP + c] = v;
-        if (g == 0 && c <= i) Lf[(int64_t)(jb + i) * PP + jb + c] = v;
-      }
-    }
-    if (lane == 0 && !ok) *flag = 1;
-  }
-  __syncthreads();
-  if (*flag) {  // every workgroup of the partition sees the same pivots
-    if (g == 0 && tid == 0) sp.state[k] = 2;
-    return;
-  }
-  const int rest = PP - jb - CB;
-  if (rest <= 0) return;
-  if (tid < rest) {  // TRSM, one row per thread
-    const double* hr = H + (int64_t)(jb + CB + tid) * PP + jb;
-    double v[CB];
-#pragma unroll
-    for (int c = 0; c < CB; ++c) v[c] = hr[c];
-#pragma unroll
-    for (int c = 0; c < CB; ++c) {
-      double s = v[c];
-#pragma unroll
-      for (int e = 0; e < c; ++e) s -= v[e] * L11[c * LDP + e];
-      v[c] = s / L11[c * LDP + c];
-    }
-    double* lr = Lf + (int64_t)(jb + CB + tid) * PP + jb;
-#pragma unroll
-    for (int c = 0; c < CB; ++c) {
-      Lp[tid * LDP + c] = v[c];
-      if (g == 0) lr[c] = v[c];
-    }
-  }
-  __syncthreads();
-  // trailing update: lower 16x16 tiles of A22, tile t to wave (t / G?) --
-  // workgroup g takes tiles g, g + G, ..., its 16 waves UT at a time
-  const int fl = lane & 15, kq = lane >> 4;
-  const int m = rest / 16;
-  const int ntiles = m * (m + 1) / 2;
-  const int wv = __builtin_amdgcn_readfirstlane(wid);
-  constexpr int UT = 4;
-  const int stride = 16 * G;
-  for (int t0 = g + G * wv; t0 < ntiles; t0 += stride * UT) {
-    int ti[UT], tj[UT];
-    d4w c[UT];
-#pragma unroll
-    for (int u = 0; u < UT; ++u) {
-      tile_ij(min(t0 + stride * u, ntiles - 1), ti[u], tj[u]);
-      const double* cp = H + (int64_t)(jb + CB + 16 * ti[u] + kq) * PP + jb + CB + 16 * tj[u] + fl;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) c[u][r] = cp[4 * r * PP];
-    }
-#pragma unroll
-    for (int u = 0; u < UT; ++u) {
-      d4w acc = d4w{0, 0, 0, 0};
-#pragma unroll
-      for (int s2 = 0; s2 < CB / 4; ++s2) {
-        const double av = Lp[(16 * ti[u] + fl) * LDP + 4 * s2 + kq];
-        const double bv = Lp[(16 * tj[u] + fl) * LDP + 4 * s2 + kq];
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
-      }
-      if (t0 + stride * u < ntiles) {
-        double* cp = H + (int64_t)(jb + CB + 16 * ti[u] + kq) * PP + jb + CB + 16 * tj[u] + fl;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) cp[4 * r * PP] = c[u][r] - acc[r];
-      }
-    }
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1422,42 +1233,14 @@ hipError_t launch_wide_assemble(const WideArgs& a, const int32_t* gcb, double* H
   return hipGetLastError();
 }
 
-// split factorization: DLSA_WIDE_SPLIT = workgroups per partition of the
-// panel kernels (0 / unset: the single-workgroup kernel); the caller passes
-// the split buffers only when wide_split_groups() > 0
-int wide_split_groups(int K) {
-  if (const char* e = getenv("DLSA_WIDE_SPLIT")) return std::max(0, atoi(e));
-  (void)K;
-  return 0;
-}
-
 hipError_t launch_wide_newton(const SolveArgs& sa, const WideArgs& wa, const int32_t* rcb,
-                              const int32_t* gcb, double* Hfull, int K, hipStream_t s,
-                              const WideSplitBuffers* split) {
-  const int lds = wide_newton_lds_bytes(wa.NB);
-  if (!split || split->groups <= 0) {
-    hipError_t e = ensure_max_lds((const void*)wide_newton_kernel<WN_ALL>, 160 * 1024);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(wide_newton_kernel<WN_ALL>, dim3(K), dim3(1024), lds, s, sa, wa, rcb, gcb,
-                       Hfull, WideSplit{nullptr, nullptr, nullptr, nullptr});
-    return hipGetLastError();
-  }
-  const WideSplit sp{split->state, split->ll, split->g, split->L};
-  for (const void* kern : {(const void*)wide_newton_kernel<WN_PRE>,
-                           (const void*)wide_newton_kernel<WN_POST>,
-                           (const void*)wide_chol_panel_kernel}) {
-    hipError_t e = ensure_max_lds(kern, 160 * 1024);
+                              const int32_t* gcb, double* Hfull, int K, hipStream_t s) {
+  {
+    hipError_t e = ensure_max_lds((const void*)wide_newton_kernel, 160 * 1024);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(wide_newton_kernel<WN_PRE>, dim3(K), dim3(1024), lds, s, sa, wa, rcb, gcb,
-                     Hfull, sp);
-  const int PP = GT * wa.NB;
-  const int lds_panel = (CB * LDP + PP * LDP + 2) * (int)sizeof(double);
-  for (int jb = 0; jb < PP; jb += CB)
-    hipLaunchKernelGGL(wide_chol_panel_kernel, dim3(split->groups, K), dim3(1024), lds_panel, s,
-                       wa, Hfull, sp, jb);
-  hipLaunchKernelGGL(wide_newton_kernel<WN_POST>, dim3(K), dim3(1024), lds, s, sa, wa, rcb, gcb,
-                     Hfull, sp);
+  hipLaunchKernelGGL(wide_newton_kernel, dim3(K), dim3(1024), wide_newton_lds_bytes(wa.NB), s,
+                     sa, wa, rcb, gcb, Hfull);
   return hipGetLastError();
 }
 

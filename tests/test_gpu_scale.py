@@ -113,6 +113,37 @@ def test_config3_partition_size(torch_cuda, M):
         assert _rel(fit.sig_inv[k].cpu(), o["Sig_inv"]) < REL
 
 
+def test_config3_reference_partition_policy(torch_cuda, M):
+    """Config 3 at the reference's own partition policy: K = ceil(n / 1e6)
+    and row % K (projects/logistic_dlsa.py:170, 239-245), i.e. partitions of
+    1e6 rows of the airline-like categorical layout (P = 182).  Partition 0
+    against the oracle on its dense dummy expansion (1e6 x 182), partition 1
+    through the score equation on the device."""
+    torch = torch_cuda
+    n = 2_000_000
+    K = -(-n // 1_000_000)  # ceil(n / 1e6), logistic_dlsa.py:239-240
+    Xn, codes, y, levels = M.simulate_categorical(n, seed=7, device="cuda")
+    # row % K then grouped (repartition + groupby): partition k = rows k, k+K, ...
+    order = torch.cat([torch.arange(k, n, K, device="cuda") for k in range(K)])
+    Xn, codes, y = Xn[order].contiguous(), codes[order].contiguous(), y[order].contiguous()
+    off = np.array([0] + [len(range(k, n, K)) for k in range(K)], dtype=np.int64).cumsum()
+    assert (np.diff(off) == 1_000_000).all()
+    fit = M.logistic_model_batched_categorical(Xn, codes, y, off, levels, fit_intercept=True)
+    assert (fit.status.cpu().numpy() == 0).all(), fit.status_counts()
+    Xd = M.expand_categorical(Xn, codes, levels)
+    Xd = torch.cat([torch.ones((n, 1), dtype=torch.float64, device=Xd.device), Xd], 1)
+    a, b = int(off[1]), int(off[2])
+    g = Xd[a:b].T @ (y[a:b] - torch.sigmoid(Xd[a:b] @ fit.theta[1]))
+    assert g.abs().max().item() < 1e-4  # Sum w over 1e6 rows ~ 2e5: 1e-4 ~ 5e-10 rel
+    a, b = int(off[0]), int(off[1])
+    Xh = Xd[a:b].cpu().numpy()
+    yh = y[a:b].cpu().numpy()
+    del Xd
+    o = O.logistic_fit(Xh, yh)  # intercept column already in Xh
+    assert _rel(fit.theta[0].cpu(), o["coef"]) < REL
+    assert _rel(fit.sig_inv[0].cpu(), o["Sig_inv"]) < REL
+
+
 def test_config4_partition_size(torch_cuda, M):
     """BASELINE config 4 (OLS DLSA) at its partition size: p = 64, K = 8
     partitions of 976 563 rows in HBM (the bench's linear response).

@@ -19,12 +19,6 @@ for v in "$@"; do
     solveprof) D=DLSA_SOLVE_PROFILE=1 ;;
     cat31) D=DLSA_CAT_ABLATE=31 ;;
     fab1) D=DLSA_FUSED_ABLATE=1 ;;
-    wab1) D=DLSA_WAVE_ABLATE=1 ;;
-    wab2) D=DLSA_WAVE_ABLATE=2 ;;
-    zimg) D=DLSA_WAVE_ZIMG=1 ;;
-    mf4) D=DLSA_WAVE_MF4=1 ;;
-    mf4d) D=DLSA_WAVE_MF4=2 ;;
-    gmf4) D=DLSA_GRAM_MF4=1 ;;
     nt) D=DLSA_X_DMA_AUX=2 ;;
     sc1) D=DLSA_X_DMA_AUX=1 ;;
     *) echo "unknown variant $v"; exit 1 ;;
