@@ -81,27 +81,6 @@ hipError_t launch_polish_mark(int K, int32_t* phase, const int32_t* status, int3
   return hipGetLastError();
 }
 
-__global__ void stagger_kernel(int K, int32_t* phase, const int32_t* status, int32_t* counters,
-                               int from, int hold) {
-  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < K; k += gridDim.x * blockDim.x) {
-    if (status[k] != STATUS_RUNNING) continue;
-    if (hold && (k & 1) && phase[k] == from) {
-      phase[k] = PHASE_WAIT;
-      atomicSub(&counters[from], 1);
-    } else if (!hold && phase[k] == PHASE_WAIT) {
-      phase[k] = from;
-      atomicAdd(&counters[from], 1);
-    }
-  }
-}
-
-hipError_t launch_stagger(int K, int32_t* phase, const int32_t* status, int32_t* counters,
-                          int from, int hold, hipStream_t s) {
-  hipLaunchKernelGGL(stagger_kernel, dim3((K + 255) / 256), dim3(256), 0, s, K, phase, status,
-                     counters, from, hold);
-  return hipGetLastError();
-}
-
 // sig_inv_theta = Sig_inv @ theta (models.py:131); still-running -> MAXITER.
 __global__ void fit_finalize_kernel(int K, int P, const double* theta, const double* sig_inv,
                                     double* sig_inv_theta, int32_t* status) {

@@ -141,40 +141,6 @@ static int32_t* pinned_staging(size_t n_i32) {
   return buf;
 }
 
-// Second stream of the calling thread (created on first use, on the current
-// device) and a fork / join event pair: the staggered fit runs one group's
-// exact pass beside the other group's approximate pass.  Kept for the thread's
-// lifetime like pinned_staging.
-struct SideStream {
-  hipStream_t s = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-  int dev = -1;
-};
-static hipError_t side_stream(SideStream*& out) {
-  thread_local SideStream ss;
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return e;
-  if (ss.s == nullptr || ss.dev != dev) {
-    e = hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&ss.join, hipEventDisableTiming);
-    if (e != hipSuccess) return e;
-    ss.dev = dev;
-  }
-  out = &ss;
-  return hipSuccess;
-}
-
-// Staggered final level (DLSA_STAGGER=1): the odd partitions start the
-// full-data Newton one iteration late, so when the even ones take their exact
-// (MFMA-bound) pass the odd ones take their last approximate (HBM-bound) pass,
-// on a second stream, and the two overlap.
-static bool stagger_enabled() {
-  const char* e = getenv("DLSA_STAGGER");
-  return e && atoi(e) > 0;
-}
-
 static double warm_level_tol(bool fused) {
   if (const char* e = getenv("DLSA_LEVEL_TOL")) return atof(e);
   return fused ? 0.2 : 0.1;
@@ -968,22 +934,15 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
   // exact (fp64 Hessian) passes by the per-wave kernel up to P = 128 and the
   // cooperative one above; approximate passes (PHASE_F32 at the fit's
   // approximate precision, PHASE_F32X at fp32) by the cooperative kernel
-  const bool stagger = stagger_enabled() && family == FAMILY_LOGISTIC &&
-                       start_phase != PHASE_F64 && K >= 2 && max_iter >= 20;
-  SideStream* side = nullptr;
-  if (stagger) DLSA_HIP_TRY(side_stream(side));
-  StreamTimer timed_side{side ? side->s : stream, opt.record_timing != 0};
   auto fused_pass = [&](int ph, const Plan& q, const std::vector<int64_t>& part_rows,
-                        const int32_t* hph, bool on_side = false) -> hipError_t {
+                        const int32_t* hph) -> hipError_t {
     const bool f64 = ph == PHASE_F64;
     const int prec = f64 ? PREC_F64 : (ph == PHASE_F32X ? PREC_F32 : approx_prec);
     pa.want_phase = ph;
     const bool wave = f64 && q.NT <= kWaveMaxNT;
-    const hipStream_t st = on_side ? side->s : stream;
-    StreamTimer& tm = on_side ? timed_side : timed;
-    hipError_t e = tm(f64 ? &g_stats.ms_pass_fp64 : &g_stats.ms_pass_fp32, [&] {
-      if (wave) return launch_irls_wave(pa, q.NT, standardize, family, q.n_chunks, st);
-      return launch_irls_coop(pa, q.NT, prec, standardize, family, q.n_chunks, st);
+    hipError_t e = timed(f64 ? &g_stats.ms_pass_fp64 : &g_stats.ms_pass_fp32, [&] {
+      if (wave) return launch_irls_wave(pa, q.NT, standardize, family, q.n_chunks, stream);
+      return launch_irls_coop(pa, q.NT, prec, standardize, family, q.n_chunks, stream);
     });
     if (f64) {
       g_stats.passes_fp64++;
@@ -1021,37 +980,14 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
     if (it_end <= it) continue;  // no budget left for this warm-start level
     DLSA_HIP_TRY(hipMemsetAsync(sa.dm_prev, 0, 8LL * K, stream));
     DLSA_HIP_TRY(hipMemsetAsync(sa.stall, 0, 4LL * K, stream));
-    bool release = false;
-    if (stagger && final_level) {  // hold the odd partitions for one iteration
-      DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
-      DLSA_HIP_TRY(launch_stagger(K, d_phase, status, d_cnt, start_phase, 1, stream));
-      DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, stream));
-      DLSA_HIP_TRY(hipStreamSynchronize(stream));
-      n_running[start_phase] += h_cnt[start_phase];  // minus the held partitions
-      release = h_cnt[start_phase] < 0;
-    }
     for (; it < it_end && running_total(n_running) > 0 && q.n_chunks > 0; ++it) {
-      // approximate (bf16 or fp32), escalated fp32, then exact passes; with
-      // the stagger the exact pass runs on the side stream beside them
-      const bool overlap = stagger && n_running[PHASE_F64] > 0 &&
-                           (n_running[PHASE_F32] > 0 || n_running[PHASE_F32X] > 0);
-      if (overlap) {
-        DLSA_HIP_TRY(hipEventRecord(side->fork, stream));
-        DLSA_HIP_TRY(hipStreamWaitEvent(side->s, side->fork, 0));
-        DLSA_HIP_TRY(fused_pass(PHASE_F64, q, part_rows, h_phase, true));
-        DLSA_HIP_TRY(hipEventRecord(side->join, side->s));
-      }
+      // approximate (bf16 or fp32), escalated fp32, then exact passes
       for (int ph : {PHASE_F32, PHASE_F32X, PHASE_F64}) {
-        if (n_running[ph] == 0 || (overlap && ph == PHASE_F64)) continue;
+        if (n_running[ph] == 0) continue;
         DLSA_HIP_TRY(fused_pass(ph, q, part_rows, h_phase));
       }
-      if (overlap) DLSA_HIP_TRY(hipStreamWaitEvent(stream, side->join, 0));
       DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
       DLSA_HIP_TRY(timed(&g_stats.ms_solve, [&] { return launch_newton_solve(sa, K, stream); }));
-      if (release) {  // the held partitions join from the next iteration on
-        DLSA_HIP_TRY(launch_stagger(K, d_phase, status, d_cnt, start_phase, 0, stream));
-        release = false;
-      }
       DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, stream));
       DLSA_HIP_TRY(hipMemcpyAsync(h_phase, d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
       DLSA_HIP_TRY(hipStreamSynchronize(stream));
@@ -1083,7 +1019,6 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
                                                                t_start)
                          .count();
   DLSA_HIP_TRY(timed.flush());
-  DLSA_HIP_TRY(timed_side.flush());
   return DLSA_OK;
 }
 

@@ -23,11 +23,7 @@ enum : int32_t {
   PHASE_F64 = 1,
   PHASE_F32X = 2,
   PHASE_DONE = 3,
-  PHASE_LEVEL_DONE = 4,
-  // staggered start (capi.hip fit_impl): the partition sits out the first
-  // full-data iteration, so its exact pass later overlaps other partitions'
-  // approximate passes
-  PHASE_WAIT = 5
+  PHASE_LEVEL_DONE = 4
 };
 constexpr int kRunPhases = 3;
 enum : int32_t { STATUS_RUNNING = -1 };
@@ -280,10 +276,6 @@ hipError_t launch_level_reset(int K, int P, int start_phase, int32_t* phase, int
                               int32_t* counters, hipStream_t s);
 hipError_t launch_polish_mark(int K, int32_t* phase, const int32_t* status, int32_t* counters,
                               hipStream_t s);
-// stagger: hold (hold = 1) the odd running partitions in PHASE_WAIT, taking
-// them off counters[from]; release (hold = 0) them into phase `from`
-hipError_t launch_stagger(int K, int32_t* phase, const int32_t* status, int32_t* counters,
-                          int from, int hold, hipStream_t s);
 hipError_t launch_fit_finalize(int K, int P, const double* theta, const double* sig_inv,
                                double* sig_inv_theta, int32_t* status, hipStream_t s);
 hipError_t launch_reduce_partitions(const double* sig_inv, const double* sig_inv_theta,

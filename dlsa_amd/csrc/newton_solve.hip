@@ -70,7 +70,7 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
   const int k = blockIdx.x;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
-  if (a.status[k] != STATUS_RUNNING || a.phase[k] == PHASE_WAIT) return;  // block-uniform
+  if (a.status[k] != STATUS_RUNNING) return;  // block-uniform
   const int P = a.P;
   double* H = sm;                    // packed lower triangle, P (P + 1) / 2
   double* g = H + P * (P + 1) / 2;   // PP
@@ -472,7 +472,7 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
 // workgroup (config 3: 65 chunks x 78 tiles per partition).
 __global__ __launch_bounds__(256) void partials_sum_kernel(const SolveArgs a, int T, int PP) {
   const int k = blockIdx.y;
-  if (a.status[k] != STATUS_RUNNING || a.phase[k] == PHASE_WAIT) return;
+  if (a.status[k] != STATUS_RUNNING) return;
   const int cb = a.part_chunk_begin[k], n = a.part_chunk_begin[k + 1] - cb;
   if (n <= 1) return;
   const int lane = threadIdx.x & 63;
