@@ -32,6 +32,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <array>
 #include <type_traits>
 #include <utility>
 
@@ -143,6 +144,12 @@ __device__ __forceinline__ double wv_log12(double t) {
 
 }  // namespace
 
+// Ring slots per workgroup (DLSA_WAVE_NSLOT): 2 = one block in flight while
+// the current one is computed; 3 = two blocks in flight.
+#ifndef DLSA_WAVE_NSLOT
+#define DLSA_WAVE_NSLOT 2
+#endif
+constexpr int kWaveSlots = DLSA_WAVE_NSLOT;
 // Ring slot: [16 B pad][npieces KiB of X rows][256 B: y of up to 32 rows]
 __host__ __device__ __forceinline__ int wave_npieces(int RB, int p) {
   return (RB * p * 8 + 16 + 1023) / 1024;
@@ -153,7 +160,7 @@ __host__ __device__ __forceinline__ int wave_slot_bytes_impl(int RB, int p) {
 // LDS of one workgroup: 2 ring slots + w of a block [RB] + theta [PMAX] +
 // center / 1/scale [2][PMAX]
 __host__ __device__ __forceinline__ int wave_lds_bytes_impl(int NT, int RB, int p) {
-  return 2 * wave_slot_bytes_impl(RB, p) + RB * 8 + 3 * 16 * NT * 8;
+  return kWaveSlots * wave_slot_bytes_impl(RB, p) + RB * 8 + 3 * 16 * NT * 8;
 }
 
 // Waves per workgroup.  W = 2 (P <= 112): the T tiles are split over two
@@ -273,6 +280,37 @@ struct WaveTiles {
   }
 };
 
+// MFMA issue order of a wave's tiles (DLSA_WAVE_ORDER = 1): greedy, each
+// next tile taking a different A operand (tile row) AND a different B operand
+// (tile column) than the previous one where one is left -- back-to-back fp64
+// MFMAs on a shared operand register issue slower (tools/mfma_rate_probe.hip).
+// 0: tiles in row order (the rows' A operand reused back to back).
+#ifndef DLSA_WAVE_ORDER
+#define DLSA_WAVE_ORDER 0
+#endif
+template <class TL, int TW>
+struct WaveIssueOrder {
+  static constexpr std::array<int, TW> make() {
+    std::array<int, TW> ord{};
+    bool used[TW > 0 ? TW : 1] = {};
+    int pi = -1, pj = -1;
+    for (int n = 0; n < TW; ++n) {
+      int pick = -1;
+      if (DLSA_WAVE_ORDER)
+        for (int i = 0; i < TW && pick < 0; ++i)
+          if (!used[i] && TL::I_of(i) != pi && TL::J_of(i) != pj) pick = i;
+      for (int i = 0; i < TW && pick < 0; ++i)
+        if (!used[i]) pick = i;
+      used[pick] = true;
+      ord[n] = pick;
+      pi = TL::I_of(pick);
+      pj = TL::J_of(pick);
+    }
+    return ord;
+  }
+  static constexpr std::array<int, TW> ord = make();
+};
+
 template <typename F, int... Is>
 __device__ __forceinline__ void wv_static_for_impl(F&& f, std::integer_sequence<int, Is...>) {
   (f(std::integral_constant<int, Is>{}), ...);
@@ -322,7 +360,7 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
 
   const int lane = threadIdx.x & 63;
   const int p = a.p, P = a.P, ic = a.intercept;
-  double* wv = (double*)(smem + 2 * cx.slot_bytes);  // [RB] w of the block's rows
+  double* wv = (double*)(smem + kWaveSlots * cx.slot_bytes);  // [RB] w of the block's rows
   double* bet = wv + RB;                             // [PMAX] theta of the partition
   double* stdv = bet + PMAX;                         // [2][PMAX] center, 1/scale (STD)
 
@@ -348,7 +386,7 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
   for (int j = WID; j < cx.npieces; j += W) ++my_ops;
   if (WID == W - 1) ++my_ops;
   auto issue = [&](int blk) {
-    char* sbase = smem + (blk & 1) * cx.slot_bytes;
+    char* sbase = smem + (blk % kWaveSlots) * cx.slot_bytes;
     const uintptr_t start = (uintptr_t)(a.X + (cx.row0 + (int64_t)blk * RB) * p);
     const int so = __builtin_amdgcn_readfirstlane((int)((start & ~(uintptr_t)15) - cx.xcb));
     for (int j = WID; j < cx.npieces; j += W)
@@ -358,16 +396,21 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
       __builtin_amdgcn_raw_ptr_buffer_load_lds(cx.yr, (wlds_void_t*)(sbase + cx.slot_y), 4,
                                                lane * 4, blk * RB * 8, 0, 0);
   };
-  (void)my_ops;
 
   const int fl = lane & 15, q = lane >> 4;
   const bool icpt_lane = ic && fl == 0;
-  issue(0);
+  for (int b = 0; b < kWaveSlots - 1 && b < cx.nb; ++b) issue(b);
   for (int b = 0; b < cx.nb; ++b) {
-    wv_wait_vmcnt<0>();  // this wave's pieces of block b (nothing younger is issued yet)
+    // this wave's pieces of block b landed (the younger blocks' may not have)
+    if constexpr (kWaveSlots == 2) {
+      wv_wait_vmcnt<0>();
+    } else {
+      const int younger = min(kWaveSlots - 2, cx.nb - 1 - b);  // blocks issued after b
+      wv_wait_vmcnt_le<2 * 8>(younger * my_ops);
+    }
     wv_sync<W>();        // every wave's pieces landed; block b-1 fully consumed
-    if (b + 1 < cx.nb) issue(b + 1);  // into the slot of block b-1
-    const char* slot = smem + (b & 1) * cx.slot_bytes;
+    if (b + kWaveSlots - 1 < cx.nb) issue(b + kWaveSlots - 1);  // into the slot of block b-1
+    const char* slot = smem + (b % kWaveSlots) * cx.slot_bytes;
     const uintptr_t start = (uintptr_t)(a.X + (cx.row0 + (int64_t)b * RB) * p);
     double* xs = (double*)(slot + 16 + (start & 15));
     const double* ys = (const double*)(slot + cx.slot_y);
@@ -461,8 +504,8 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
 #pragma unroll
         for (int r = 0; r < NS; ++r) as[r] = OLS_NOMUL ? xso[u][r] : xso[u][r] * wk[u];
       }
-      wv_static_for<TW>([&](auto iI) {
-        constexpr int i = decltype(iI)::value;
+      wv_static_for<TW>([&](auto oI) {
+        constexpr int i = WaveIssueOrder<TL, TW>::ord[decltype(oI)::value];
         constexpr int I = TL::I_of(i), J = TL::J_of(i);
         if constexpr (strip(I)) {
 #pragma unroll
@@ -560,13 +603,13 @@ __global__ __launch_bounds__(64 * W, wave_min_waves(NT, W, FAM)) void irls_wave_
   cx.npieces = wave_npieces(RB, p);
   cx.slot_bytes = wave_slot_bytes_impl(RB, p);
   cx.slot_y = 16 + cx.npieces * 1024;
-  double* wv = (double*)(smem + 2 * cx.slot_bytes);
+  double* wv = (double*)(smem + kWaveSlots * cx.slot_bytes);
   double* bet = wv + RB;
   double* stdv = bet + PMAX;
 
   // the ring must hold finite values where no DMA lands (tails, pads): a
   // padded row reads them with w = 0, and 0 * NaN would poison the tiles
-  for (int o = tid * 16; o < 2 * cx.slot_bytes; o += 64 * W * 16)
+  for (int o = tid * 16; o < kWaveSlots * cx.slot_bytes; o += 64 * W * 16)
     *(uint4*)(smem + o) = make_uint4(0, 0, 0, 0);
   for (int f = tid; f < PMAX; f += 64 * W)
     bet[f] = (f < P) ? a.theta[(int64_t)cx.part * P + f] : 0.0;

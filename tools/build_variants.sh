@@ -19,6 +19,8 @@ for v in "$@"; do
     solveprof) D=DLSA_SOLVE_PROFILE=1 ;;
     cat31) D=DLSA_CAT_ABLATE=31 ;;
     fab1) D=DLSA_FUSED_ABLATE=1 ;;
+    wslot3) D=DLSA_WAVE_NSLOT=3 ;;
+    word) D=DLSA_WAVE_ORDER=1 ;;
     nt) D=DLSA_X_DMA_AUX=2 ;;
     sc1) D=DLSA_X_DMA_AUX=1 ;;
     *) echo "unknown variant $v"; exit 1 ;;

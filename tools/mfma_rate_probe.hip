@@ -28,7 +28,10 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 
 // 8 random operands per lane (a, b), NACC accumulators; every inner step of
 // 8 uses pair ((i + u) & 7, (3 i + u) & 7): different data every MFMA
-template <int NACC, bool BIG, bool RANDOM>
+// operand pattern of consecutive MFMAs: 0 = both A and B change every MFMA,
+// 1 = same A for runs of NACC (B changes), 2 = same B (A changes), 3 = same A
+// and B every MFMA (tools/mfma4_probe.hip's pattern)
+template <int NACC, bool BIG, bool RANDOM, int PAT = 0>
 __global__ __launch_bounds__(256) void k_rate(const double* src, double* out, long long* stamps,
                                               int iters) {
   const int lane = threadIdx.x;
@@ -52,12 +55,12 @@ __global__ __launch_bounds__(256) void k_rate(const double* src, double* out, lo
     for (int u = 0; u < 8; ++u)
 #pragma unroll
       for (int i = 0; i < NACC; ++i) {
+        const int ia = PAT == 0 ? (i + u) & 7 : PAT == 1 ? u : PAT == 2 ? (i + u) & 7 : 0;
+        const int ib = PAT == 0 ? (3 * i + u) & 7 : PAT == 1 ? (3 * i + u) & 7 : PAT == 2 ? u : 0;
         if constexpr (BIG)
-          acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[(i + u) & 7], b[(3 * i + u) & 7], acc[i],
-                                                        0, 0, 0);
+          acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ia], b[ib], acc[i], 0, 0, 0);
         else
-          acc4[i] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[(i + u) & 7], b[(3 * i + u) & 7], acc4[i],
-                                                       0, 0, 0);
+          acc4[i] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[ia], b[ib], acc4[i], 0, 0, 0);
       }
   }
   const long long t1 = __builtin_amdgcn_s_memtime();
@@ -117,6 +120,13 @@ int main() {
            name, wps, sec * 1e9 / per_simd, tf, clk[g / 2], sec * 1e9 / per_simd * clk[g / 2]);
     return 0;
   };
+  for (int wps : {2}) {
+    if (run(k_rate<8, true, true, 1>, 8, 2048.0, wps, "f64 16x16x4 same A in runs of 8")) return 1;
+    if (run(k_rate<8, true, true, 2>, 8, 2048.0, wps, "f64 16x16x4 same B in runs of 8")) return 1;
+    if (run(k_rate<8, true, true, 3>, 8, 2048.0, wps, "f64 16x16x4 same A and B always")) return 1;
+    if (run(k_rate<12, true, true, 0>, 12, 2048.0, wps, "f64 16x16x4 12 acc, A and B change")) return 1;
+    if (run(k_rate<12, true, true, 1>, 12, 2048.0, wps, "f64 16x16x4 12 acc, same A runs of 12")) return 1;
+  }
   for (int wps : {1, 2}) {
     if (run(k_rate<8, true, false>, 8, 2048.0, wps, "f64 16x16x4 constant operands")) return 1;
     if (run(k_rate<8, true, true>, 8, 2048.0, wps, "f64 16x16x4 random operands")) return 1;
