@@ -506,7 +506,8 @@ def main():
         "stages_ms_per_step": dict({k: v / args.steps for k, v in stage_ms.items()},
                                    fit_native=tot("ms_total") / args.steps),
         "newton": {"iterations": last["iterations"], "passes_fp32": last["passes_fp32"],
-                   "passes_fp64": last["passes_fp64"], "n_chunks": last["n_chunks"],
+                   "passes_fp64": last["passes_fp64"], "passes_oz": last.get("passes_oz", 0),
+                   "n_chunks": last["n_chunks"],
                    "status": fit.status_counts()},
         "dbic_support_size": int(len(support)),
         "algorithmic": {"bytes_per_pass": n * row_bytes, "flops_per_pass": n * alg_flops_row},

@@ -60,6 +60,7 @@ class FitStats(ctypes.Structure):
         ("ms_wide_assemble", ctypes.c_double),
         ("passes_f32x", ctypes.c_int32),
         ("polish_partitions", ctypes.c_int32),
+        ("passes_oz", ctypes.c_int32),
     ]
 
     def as_dict(self):

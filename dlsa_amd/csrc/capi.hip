@@ -53,6 +53,7 @@ static inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * 
 struct Plan {
   int P = 0, NT = 0, T = 0, PP = 0;
   int n_chunks = 0;
+  int max_chunk_rows = 0;
   std::vector<int64_t> chunk_row0;
   std::vector<int32_t> chunk_rows, chunk_part, part_chunk_begin;
 };
@@ -182,6 +183,8 @@ static bool make_plan(const int64_t* offsets, int K, int p, int intercept, int r
   }
   pl.part_chunk_begin[K] = (int32_t)pl.chunk_row0.size();
   pl.n_chunks = (int)pl.chunk_row0.size();
+  pl.max_chunk_rows = 0;
+  for (int32_t r : pl.chunk_rows) pl.max_chunk_rows = std::max<int>(pl.max_chunk_rows, r);
   return true;
 }
 
@@ -190,6 +193,7 @@ struct Layout {
   int64_t off_slabH, off_slabg, off_slabll;
   int64_t off_phase, off_bt, off_llprev, off_thprev, off_dprev, off_counters;
   int64_t off_dmprev, off_stall;
+  int64_t off_colmax;
   int64_t total;
 };
 
@@ -217,6 +221,7 @@ static Layout make_layout(const Plan& pl, int K) {
   L.off_counters = take(16);
   L.off_dmprev = take(8LL * K);
   L.off_stall = take(4LL * K);
+  L.off_colmax = take(4LL * std::max(pl.n_chunks, 1) * pl.PP);
   L.total = o;
   return L;
 }
@@ -930,6 +935,15 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
 
   const bool trace = getenv("DLSA_TRACE") != nullptr;
   int32_t* h_phase = h_cnt + 4;  // [K] phases (pinned: no staging copy per iteration)
+  // exact passes on the int8 matrix cores (irls_oz_impl.hpp) unless DLSA_OZ=0:
+  // the fit's first full-data bf16 pass records every chunk's per-feature max
+  // |x| (the digit scales), after which the exact passes of the final plan
+  // take the Ozaki kernel
+  const bool use_oz = !(getenv("DLSA_OZ") && atoi(getenv("DLSA_OZ")) == 0) &&
+                      approx_prec == PREC_BF16 && oz_applies(pl.NT, p) &&
+                      pl.max_chunk_rows <= kOzMaxRows;
+  uint32_t* d_colmax = (uint32_t*)at(L.off_colmax);
+  bool colmax_ready = false;
   // one pass over the chunks of plan q whose partition is in phase ph:
   // exact (fp64 Hessian) passes by the per-wave kernel up to P = 128 and the
   // cooperative one above; approximate passes (PHASE_F32 at the fit's
@@ -940,10 +954,19 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
     const int prec = f64 ? PREC_F64 : (ph == PHASE_F32X ? PREC_F32 : approx_prec);
     pa.want_phase = ph;
     const bool wave = f64 && q.NT <= kWaveMaxNT;
+    const bool full = &q == &plans.back();
+    const bool oz = wave && use_oz && colmax_ready && full;
+    // the first full-data bf16 pass records the digit scales
+    const bool record = use_oz && !colmax_ready && full && ph == PHASE_F32;
     hipError_t e = timed(f64 ? &g_stats.ms_pass_fp64 : &g_stats.ms_pass_fp32, [&] {
-      if (wave) return launch_irls_wave(pa, q.NT, standardize, family, q.n_chunks, stream);
-      return launch_irls_coop(pa, q.NT, prec, standardize, family, q.n_chunks, stream);
+      PassArgs pc = pa;
+      pc.colmax = (oz || record) ? d_colmax : nullptr;
+      if (oz) return launch_irls_oz(pc, q.NT, standardize, family, q.n_chunks, stream);
+      if (wave) return launch_irls_wave(pc, q.NT, standardize, family, q.n_chunks, stream);
+      return launch_irls_coop(pc, q.NT, prec, standardize, family, q.n_chunks, stream);
     });
+    if (record) colmax_ready = true;
+    if (oz) g_stats.passes_oz++;
     if (f64) {
       g_stats.passes_fp64++;
       g_stats.rows_fp64 += phase_rows(part_rows, hph, ph);

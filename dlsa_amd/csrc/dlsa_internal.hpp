@@ -63,6 +63,10 @@ struct PassArgs {
   int32_t want_phase;
   int32_t nslot;              // cooperative pass: LDS ring depth (32-row slots)
   int32_t slot_bytes;
+  // [n_chunks, 16*NT] per chunk and feature, max |x| (its fp64 high dword, after
+  // standardisation): written by a bf16 pass when set, read by the Ozaki
+  // exact pass (irls_oz_impl.hpp) as its digit scales
+  uint32_t* colmax;
 };
 
 // Arguments of the per-partition Newton update.
@@ -262,6 +266,13 @@ hipError_t launch_irls_wave(const PassArgs& a, int NT, bool standardize, int fam
                             hipStream_t s);
 int wave_lds_bytes(int NT, int p);
 constexpr int kWaveMaxNT = 8;
+// Ozaki-scheme exact pass (irls_oz_impl.hpp): NT <= kOzMaxNT, chunks <= kOzMaxRows rows;
+// a.nslot = oz_nslot(NT, p) ring slots
+hipError_t launch_irls_oz(const PassArgs& a, int NT, bool standardize, int family, int n_chunks,
+                          hipStream_t s);
+bool oz_applies(int NT, int p);  // NT <= kOzMaxNT, image and 6-slot ring fit
+constexpr int kOzMaxRows = 32767;
+constexpr int kOzMaxNT = 7;
 hipError_t launch_irls_coop(const PassArgs& a, int NT, int prec, bool standardize, int family,
                             int n_chunks, hipStream_t s);
 int coop_slot_bytes(int NT, int p);

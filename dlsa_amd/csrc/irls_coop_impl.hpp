@@ -264,7 +264,10 @@ __device__ __forceinline__ void store_tiles(Acc (&acc)[(CG<NT, W>::TPW)], double
   });
 }
 
-template <int NT, int W, int PREC, bool STD, int FAM>
+// CM: also record the chunk's per-feature max |x| into a.colmax (the first
+// full-data bf16 pass of a fit; the Ozaki exact pass takes its digit scales
+// from it)
+template <int NT, int W, int PREC, bool STD, int FAM, bool CM = false>
 __global__ __launch_bounds__(64 * W, (W == 8 || NT < 8) ? 2 : 1)
 void irls_coop_kernel(const PassArgs a) {
   using G = CG<NT, W>;
@@ -316,6 +319,9 @@ void irls_coop_kernel(const PassArgs a) {
 #pragma unroll
   for (int m = 0; m < M; ++m) asm volatile("" : "+v"(beta[m]));
   double llacc = 0.0;
+  uint32_t cmx[CM ? M : 1];  // CM: running max of |x| high dwords per feature
+#pragma unroll
+  for (int m = 0; m < (CM ? M : 1); ++m) cmx[m] = 0u;
   int tI[G::TPW], tJ[G::TPW];  // this wave's tiles (bf16 path)
 #pragma unroll
   for (int i = 0; i < G::TPW; ++i) {
@@ -394,6 +400,7 @@ void irls_coop_kernel(const PassArgs a) {
         if constexpr (STD) v = (v - stdv[sl + LPR * m]) * stdv[G::PMAX + sl + LPR * m];
         if (m == 0 && ic && sl == 0) v = 1.0;
         xv[m] = v;
+        if constexpr (CM) cmx[m] = max(cmx[m], valid ? (__double2hiint(v) & 0x7FFFFFFFu) : 0u);
         if (m & 1)
           e1 = fma(v, beta[m], e1);
         else
@@ -511,11 +518,29 @@ void irls_coop_kernel(const PassArgs a) {
     for (int w = 0; w < W; ++w) s += red[W * G::PMAX + w];
     a.slab_ll[chunk] = s;
   }
+  if constexpr (CM) {
+    __syncthreads();  // red is reused
+    uint32_t* cred = (uint32_t*)smem;  // [W][PMAX]
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      uint32_t v = cmx[m];
+#pragma unroll
+      for (int o = 1; o < RPW; o <<= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+      if (lane % RPW == 0) cred[wid * G::PMAX + sl + LPR * m] = v;
+    }
+    __syncthreads();
+    for (int f = tid; f < G::PMAX; f += 64 * W) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int w = 0; w < W; ++w) v = max(v, cred[w * G::PMAX + f]);
+      a.colmax[(int64_t)chunk * G::PMAX + f] = v;
+    }
+  }
 }
 
-template <int NT, int W, int PREC, bool STD, int FAM>
+template <int NT, int W, int PREC, bool STD, int FAM, bool CM = false>
 static hipError_t launch_c(const PassArgs& a, int n_chunks, hipStream_t s) {
-  auto kern = irls_coop_kernel<NT, W, PREC, STD, FAM>;
+  auto kern = irls_coop_kernel<NT, W, PREC, STD, FAM, CM>;
   const size_t lds =
       (size_t)a.nslot * a.slot_bytes + coop_extra_bytes_impl(NT);
   hipError_t e = ensure_max_lds((const void*)kern, 160 * 1024);
@@ -534,6 +559,11 @@ static hipError_t launch_coop_ntw(const PassArgs& a, int prec, bool std_, int fa
   }
   switch (prec) {
     case PREC_BF16:
+      if constexpr (NT <= kOzMaxNT) {
+        if (a.colmax)
+          return std_ ? launch_c<NT, W, PREC_BF16, true, FAMILY_LOGISTIC, true>(a, n_chunks, s)
+                      : launch_c<NT, W, PREC_BF16, false, FAMILY_LOGISTIC, true>(a, n_chunks, s);
+      }
       return std_ ? launch_c<NT, W, PREC_BF16, true, FAMILY_LOGISTIC>(a, n_chunks, s)
                   : launch_c<NT, W, PREC_BF16, false, FAMILY_LOGISTIC>(a, n_chunks, s);
     case PREC_F32:

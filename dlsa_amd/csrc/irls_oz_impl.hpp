@@ -1,0 +1,671 @@
+// Exact (fp64-accurate) IRLS pass on the int8 matrix cores (gfx950 / CDNA4):
+// X^T W X by integer digit slices (the Ozaki scheme), the gradient and the
+// log-likelihood in fp64.  Instantiated by irls_oz.hip / irls_oz_g2.hip.
+//
+// Replaces, per exact Newton iteration, the per-partition work of the
+// reference map stage -- sklearn newton-cg's Hessian, predict_proba and
+// Sig_inv = X^T diag(p(1-p)) X (dlsa/models.py:110-131) -- with ONE pass over
+// X, like irls_wave_impl.hpp, but without the fp64 MFMA: on gfx950 a
+// v_mfma_f64_16x16x4 issues every ~70 cycles per SIMD (72 TF/s,
+// profiles/r03h_mfma_rate_probe.txt) and fp64 VALU work never overlaps it, so
+// the fp64 pass is MFMA-bound at ~2x the HBM time of its 808 B/row (config 2:
+// 24 ms against the 14 ms of a bf16 pass).  A v_mfma_i32_16x16x64_i8 issues
+// every 16 cycles and accumulates exactly in int32.
+//
+// Numerics.  z = sqrt(w) x (the fp64 row weight times the
+// fp64 feature).  Per chunk and feature f an exponent E_f with |z_f| < 2^E_f
+// for every row of the chunk, from the chunk's max |x_f| that the fit's first
+// full-data bf16 pass recorded (PassArgs::colmax; sqrt(w) <= 1/2).
+// F = round(z 2^(38 - E_f)), |F| < 2^38, by ONE fp64 FMA against
+// 1.5 2^52 + B (B = 0x8080808080): the low 40 mantissa bits of the result are
+// F + B, whose five bytes XOR 0x80 are the balanced signed digits d_0 (most
+// significant) .. d_4 of F = sum_s d_s 2^(8(4-s)).  Then
+//   sum_rows F_i F_j = 2^64 sum_k 2^(-8k) L_k,  L_k = sum_{a+b=k} sum_rows d_a(i) d_b(j),
+// keeping the levels k < NL: H_ij = 2^(E_i + E_j - 12) sum_{k<NL} 2^(-8k) L_k.
+// The integer sums are exact and order-free; the error is the rounding of z
+// to 38 bits below 2^E_f and the dropped levels (~2^(-8 NL) of a row's leading
+// product, random in sign): ~1e-11 relative at NL = 5 (profiles/r03i), within
+// the path's 1e-8 tolerance by three orders (tests/test_gpu_parity.py).
+//
+// MFMA pairing.  One v_mfma_i32_16x16x64_i8 sums 64 k slots; a 32-row block
+// fills them with TWO digit products: lane group g holds the 8 rows of
+// producer wave g, bytes 0-7 of its fragment digit a (A features) / b (B
+// features), bytes 8-15 digit a+1 / b-1 -- both products of level a+b.  A and
+// B fragments of one lane hold the same k slots, so this needs no knowledge
+// of the instruction's k order.  a in {0, 2, 4}: 9 MFMAs per tile per 32 rows
+// cover the 15 products of levels 0-4 (out-of-range digits are zeroed in the
+// register).
+//
+// Workgroup = 4 producer + 4 consumer waves, one workgroup per CU; an
+// iteration is two 32-row blocks (b0 = 2m, b1 = 2m + 1):
+//   producers: the row phase of both blocks, interleaved (8 rows per wave per
+//     block, 8 lanes per row: eta, w, r, log-lik, gradient in fp64 -- two
+//     independent dependency chains per wave), then the digits of those rows
+//     straight from the registers: the 4 rows of a DPP quad are byte-transposed
+//     (2 quad_perm moves + 2 v_perm per dword), so lane j of a quad writes
+//     digit plane 4-j of its feature for 4 rows as one dword.  The image of a
+//     wave's 8 rows (5 planes x 16 NT features x 8 bytes) is written over those
+//     rows' own x bytes in the ring slot, once they are read;
+//   consumers: the DMA of the next iteration's two blocks (LDS-DMA, 6-slot
+//     ring), then the lower-triangle 16x16 tiles of X^T W X by column strips
+//     from the previous iteration's two images, NL int32 level accumulators
+//     per tile in registers.
+// One barrier per iteration.
+#pragma once
+
+#include <stdint.h>
+#include <stdlib.h>
+
+#include <array>
+#include <utility>
+
+#include "irls_wave_impl.hpp"
+
+namespace dlsa {
+
+typedef int oz_i4 __attribute__((ext_vector_type(4)));
+
+namespace ozk {
+
+constexpr int NPW = 4;           // producer waves
+constexpr int NCW = 4;           // consumer waves
+constexpr int RB = 32;           // rows per DMA block
+constexpr int RPW = RB / NPW;    // rows per producer wave per block (8)
+constexpr int LPR = 64 / RPW;    // row-phase lanes per row (8)
+constexpr int NSLOT = 6;         // ring: 2 in flight, 2 producing, 2 consuming
+constexpr int ND = 5;            // digits
+// levels k = a + b of digit products kept (DLSA_OZ_LEVELS: 5, 6 or 7)
+#ifndef DLSA_OZ_LEVELS
+#define DLSA_OZ_LEVELS 5
+#endif
+constexpr int NL = DLSA_OZ_LEVELS;
+static_assert(NL >= 5 && NL <= 7, "5, 6 or 7 levels");
+constexpr int EMIN = -985;       // 2^(38 - EMIN) stays finite
+constexpr int EMAX = 1023;
+// 1.5 2^52 + 0x8080808080: t = fma(x, c, MAGIC) holds F + B in its low 40 bits
+constexpr double MAGIC = 6755399441055744.0 + 551911719040.0;
+
+// Ring slot: [16 B pad][x: the block's bytes from its 16-B-aligned start][y: 256 B].
+// The x span is cut to what the block needs (the last 1-KiB DMA piece runs
+// with only the lanes inside it), so six slots of p = 100 fit the CU.
+__host__ __device__ constexpr int xspan(int p) { return (RB * p * 8 + 16 + 15) & ~15; }
+__host__ __device__ constexpr int npieces(int p) { return (xspan(p) + 1023) / 1024; }
+__host__ __device__ constexpr int slot_bytes(int p) { return 16 + xspan(p) + 256; }
+// a wave's image: [feature][digit plane][8 rows] bytes, 48 B per feature (5
+// planes + an unwritten sixth), so a lane's operand pair of planes (a, a+1),
+// a even, is one aligned 16-byte read
+constexpr int kFeatBytes = 48;
+// consumers issue the next blocks' DMA one piece per tile (1) or all before
+// their MFMAs (0)
+#ifndef DLSA_OZ_TICK
+#define DLSA_OZ_TICK 1
+#endif
+// consumers at s_setprio DLSA_OZ_PRIO: the younger half of the workgroup
+// otherwise gets only the producers' leftover issue slots (MI355X_MICROARCH.md
+// "Two waves per SIMD", items 2 and 4)
+#ifndef DLSA_OZ_PRIO
+#define DLSA_OZ_PRIO 1
+#endif
+// profiling-only ablations: 1 producers skip the row phase and digits, 2
+// consumers skip the MFMAs
+#ifndef DLSA_OZ_ABLATE
+#define DLSA_OZ_ABLATE 0
+#endif
+__host__ __device__ constexpr int img_bytes(int NT) { return 16 * NT * kFeatBytes; }
+// LDS after the ring: theta, center / 1/scale [PMAX] fp64, digit exponents [PMAX]
+__host__ __device__ constexpr int extra_bytes(int NT) { return 3 * 16 * NT * 8 + 16 * NT * 4; }
+__host__ __device__ constexpr int lds_bytes(int NT, int p) {
+  return NSLOT * slot_bytes(p) + extra_bytes(NT);
+}
+// the pass applies when a wave's image (+ skew) fits in the x bytes of its 8
+// rows and the ring fits the CU
+__host__ __device__ constexpr bool fits(int NT, int p) {
+  return img_bytes(NT) <= RPW * p * 8 && lds_bytes(NT, p) <= 160 * 1024;
+}
+
+// Column strips J (tiles (I, J), I = J .. NT-1) dealt to the consumer waves,
+// largest first, each to the wave with the fewest tiles (NT = 7: {0}, {1, 6},
+// {2, 5}, {3, 4}: 7 tiles each).
+constexpr unsigned strip_mask(int NT, int cw) {
+  int load[NCW] = {0, 0, 0, 0};
+  unsigned m[NCW] = {0, 0, 0, 0};
+  for (int J = 0; J < NT; ++J) {
+    int best = 0;
+    for (int w = 1; w < NCW; ++w)
+      if (load[w] < load[best]) best = w;
+    load[best] += NT - J;
+    m[best] |= 1u << J;
+  }
+  return m[cw];
+}
+
+template <int NT, int CW>
+struct Tiles {
+  static constexpr unsigned SM = strip_mask(NT, CW);
+  static constexpr int count() {
+    int c = 0;
+    for (int J = 0; J < NT; ++J)
+      if ((SM >> J) & 1u) c += NT - J;
+    return c;
+  }
+  static constexpr int TW = count();
+  // tile index of (I, J) in this wave (strips ascending, I ascending)
+  static constexpr int index(int I, int J) {
+    int c = 0;
+    for (int j = 0; j < NT; ++j)
+      if ((SM >> j) & 1u) {
+        if (j == J) return c + (I - J);
+        c += NT - j;
+      }
+    return -1;
+  }
+  static constexpr int I_of(int i) {
+    for (int j = 0; j < NT; ++j)
+      if ((SM >> j) & 1u) {
+        if (i < NT - j) return j + i;
+        i -= NT - j;
+      }
+    return -1;
+  }
+  static constexpr int J_of(int i) {
+    for (int j = 0; j < NT; ++j)
+      if ((SM >> j) & 1u) {
+        if (i < NT - j) return j;
+        i -= NT - j;
+      }
+    return -1;
+  }
+  static constexpr int strip_ordinal(int J) {  // strips of this wave before J
+    int c = 0;
+    for (int j = 0; j < J; ++j) c += (SM >> j) & 1u;
+    return c;
+  }
+};
+
+__device__ __forceinline__ void barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// v_perm_b32: byte s of the result = byte sel_s of {a (bytes 4-7), b (0-3)}
+__device__ __forceinline__ uint32_t perm(uint32_t a, uint32_t b, uint32_t sel) {
+  return __builtin_amdgcn_perm(a, b, sel);
+}
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+// 4x4 byte transpose across a DPP quad: lane j of the quad ends with byte j
+// of the four lanes' v (lane order = byte order).  sel1 / sel2: the lane's
+// v_perm selectors (by lane & 1, lane & 2).
+__device__ __forceinline__ uint32_t quad_transpose(uint32_t v, uint32_t sel1, uint32_t sel2) {
+  const uint32_t s1 = perm(dpp<0xB1>(v), v, sel1);  // quad_perm [1,0,3,2]: swap with lane ^ 1
+  return perm(dpp<0x4E>(s1), s1, sel2);             // quad_perm [2,3,0,1]: swap with lane ^ 2
+}
+
+// sum_k 2^(-8k) L_k of one accumulator element
+__device__ __forceinline__ double level_value(const oz_i4 (&L)[NL], int r) {
+  double v = (double)L[NL - 1][r];
+#pragma unroll
+  for (int k = NL - 2; k >= 0; --k) v = fma(v, 0x1p-8, (double)L[k][r]);
+  return v;
+}
+
+// digit exponent of a feature from its recorded max |x| high dword: the
+// bound with the low dword all ones, times 1/2 (sqrt(w) <= 1/2) for the
+// logistic family
+__device__ __forceinline__ int digit_exponent(uint32_t hi, int fam_logistic) {
+  const double bound = __hiloint2double((int)(hi & 0x7FFFFFFFu), (int)0xFFFFFFFFu);
+  int e = __builtin_amdgcn_frexp_exp(bound) - fam_logistic;
+  return min(max(e, EMIN), EMAX);
+}
+
+}  // namespace ozk
+
+// Profiling build (DLSA_OZ_PROF, tools/build_variants.sh ozprof): per-wave
+// cycle stamps (s_memtime) of the iteration's phases, summed over the chunk
+// and added to g_oz_prof[slot] at its end (one vector atomic per wave).
+#ifdef DLSA_OZ_PROF
+static __device__ unsigned long long g_oz_prof[16];  // per translation unit
+static inline int oz_prof_read_impl(unsigned long long* out) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_oz_prof), 16 * 8) != hipSuccess) return -1;
+  unsigned long long z[16] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_oz_prof), z, 16 * 8) == hipSuccess ? 0 : -1;
+}
+#define OZ_STAMP(v) const uint64_t v = __builtin_readcyclecounter()
+#define OZ_ADD(i, d) prof[i] += (d)
+#define OZ_DECL uint64_t prof[6] = {0, 0, 0, 0, 0, 0}
+#define OZ_FLUSH(base)                                                        \
+  if (lane == 0)                                                              \
+    for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&g_oz_prof[(base) + i_], prof[i_])
+#else
+#define OZ_STAMP(v)
+#define OZ_ADD(i, d)
+#define OZ_DECL
+#define OZ_FLUSH(base)
+#endif
+
+// ---- consumer waves: tiles of X^T W X -------------------------------------
+template <int NT, int CW>
+struct OzConsumer {
+  using TL = ozk::Tiles<NT, CW>;
+  static constexpr int TW = TL::TW;
+  static constexpr int PMAX = 16 * NT;
+  static constexpr int NB = ozk::NL > 5 ? 6 : 5;  // B quads
+  oz_i4 acc[TW > 0 ? TW : 1][ozk::NL];
+
+  __device__ __forceinline__ void init() {
+    wv_static_for<(TW > 0 ? TW : 1)>([&](auto iI) {
+      constexpr int i = decltype(iI)::value;
+#pragma unroll
+      for (int k = 0; k < ozk::NL; ++k) acc[i][k] = oz_i4{0, 0, 0, 0};
+    });
+  }
+
+  // the image of one 32-row block whose x started at xs (LDS); tick() is
+  // called after every tile's MFMAs (the DMA of the next blocks rides along).
+  // Software-pipelined: the operands of tile t+1 (and of the next strip) are
+  // read while the MFMAs of tile t issue.
+  template <typename Tick>
+  __device__ __forceinline__ void consume(const char* xs, int p, int lane, Tick&& tick) {
+    if constexpr (TW > 0) {
+      const int i = lane & 15, g = lane >> 4;
+      // lane group g: the image of producer wave g (its 8 rows of the block)
+      const char* im = xs + g * ozk::RPW * p * 8 + i * ozk::kFeatBytes;
+      using u2 = unsigned __attribute__((ext_vector_type(2)));
+      oz_i4 A0[2], A2[2];
+      u2 A4[2];
+      u2 Bd[2][ozk::ND];
+      auto loadB = [&](auto jJ, int u) {
+        constexpr int fo = 16 * decltype(jJ)::value * ozk::kFeatBytes;
+#pragma unroll
+        for (int b = 0; b < ozk::ND; ++b) Bd[u][b] = *(const u2*)(im + fo + 8 * b);
+      };
+      auto loadA = [&](auto tI, int u) {
+        constexpr int fa = 16 * TL::I_of(decltype(tI)::value) * ozk::kFeatBytes;
+        // A quad a: digits (a, a+1) of the feature -- one 16-byte read
+        A0[u] = *(const oz_i4*)(im + fa);
+        A2[u] = *(const oz_i4*)(im + fa + 16);
+        A4[u] = *(const u2*)(im + fa + 32);
+      };
+      loadB(std::integral_constant<int, TL::J_of(0)>{}, 0);
+      loadA(std::integral_constant<int, 0>{}, 0);
+      wv_static_for<TW>([&](auto tI) {
+        constexpr int t = decltype(tI)::value;
+        constexpr int J = TL::J_of(t);
+        constexpr int ua = t & 1;
+        constexpr int ub = TL::strip_ordinal(J) & 1;
+        if constexpr (t + 1 < TW) {
+          constexpr int Jn = TL::J_of(t + 1);
+          if constexpr (Jn != J) loadB(std::integral_constant<int, Jn>{}, ub ^ 1);
+          loadA(std::integral_constant<int, t + 1>{}, ua ^ 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // B quad b: bytes 0-7 digit b, bytes 8-15 digit b - 1 (zero for b = 0)
+        const u2* d = Bd[ub];
+        oz_i4 Bq[NB];
+        Bq[0] = oz_i4{(int)d[0].x, (int)d[0].y, 0, 0};
+#pragma unroll
+        for (int b = 1; b < ozk::ND; ++b)
+          Bq[b] = oz_i4{(int)d[b].x, (int)d[b].y, (int)d[b - 1].x, (int)d[b - 1].y};
+        if constexpr (NB > 5) Bq[5] = oz_i4{0, 0, (int)d[4].x, (int)d[4].y};
+        const oz_i4 a0 = A0[ua], a2 = A2[ua];
+        const oz_i4 a4 = oz_i4{(int)A4[ua].x, (int)A4[ua].y, 0, 0};  // digit 5 = 0
+        acc[t][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, Bq[0], acc[t][0], 0, 0, 0);
+        acc[t][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, Bq[1], acc[t][1], 0, 0, 0);
+        acc[t][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, Bq[2], acc[t][2], 0, 0, 0);
+        acc[t][3] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, Bq[3], acc[t][3], 0, 0, 0);
+        acc[t][4] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, Bq[4], acc[t][4], 0, 0, 0);
+        acc[t][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a2, Bq[0], acc[t][2], 0, 0, 0);
+        acc[t][3] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a2, Bq[1], acc[t][3], 0, 0, 0);
+        acc[t][4] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a2, Bq[2], acc[t][4], 0, 0, 0);
+        acc[t][4] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a4, Bq[0], acc[t][4], 0, 0, 0);
+        if constexpr (ozk::NL > 5) {  // level 5: (1,4) (2,3) (3,2) (4,1)
+          acc[t][5] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, Bq[NB - 1], acc[t][5], 0, 0, 0);
+          acc[t][5] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a2, Bq[3], acc[t][5], 0, 0, 0);
+          acc[t][5] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a4, Bq[1], acc[t][5], 0, 0, 0);
+        }
+        if constexpr (ozk::NL > 6) {  // level 6: (2,4) (3,3) (4,2)
+          acc[t][6] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a2, Bq[4], acc[t][6], 0, 0, 0);
+          acc[t][6] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a4, Bq[2], acc[t][6], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        tick();
+      });
+      // keep the level accumulators in registers across the loop
+      wv_static_for<TW>([this](auto iI) {
+        constexpr int t = decltype(iI)::value;
+#pragma unroll
+        for (int k = 0; k < ozk::NL; ++k) asm volatile("" : "+v"(acc[t][k]));
+      });
+    }
+  }
+
+  // H tiles into the chunk's slab (newton_solve.hip layout), scaled back
+  __device__ __forceinline__ void store(double* sH, const int* ex, int lane) {
+    if constexpr (TW > 0) {
+      const int fl = lane & 15, q = lane >> 4;
+      wv_static_for<TW>([&](auto iI) {
+        constexpr int t = decltype(iI)::value;
+        constexpr int I = TL::I_of(t), J = TL::J_of(t);
+        constexpr int ts = I * (I + 1) / 2 + J;
+        const int ej = ex[16 * J + fl];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {  // i32 16x16 C/D map: row 4 (l >> 4) + r, col l & 15
+          const int row = 4 * q + r;
+          const double v = ozk::level_value(acc[t], r);
+          sH[ts * 256 + row * 16 + fl] = __builtin_amdgcn_ldexp(v, ej + ex[16 * I + row] - 12);
+        }
+      });
+    }
+  }
+};
+
+template <int NT, bool STD, int FAM>
+__global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(const PassArgs a) {
+  using namespace ozk;
+  constexpr int PMAX = 16 * NT;
+  constexpr int M = PMAX / LPR;  // row-phase features per lane
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int chunk = blockIdx.x;
+  const int part = __builtin_amdgcn_readfirstlane(a.chunk_part[chunk]);
+  if (a.phase[part] != a.want_phase) return;  // workgroup-uniform
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int p = a.p, P = a.P, ic = a.intercept;
+  const int64_t row0 =
+      ((int64_t)__builtin_amdgcn_readfirstlane((int)(a.chunk_row0[chunk] >> 32)) << 32) |
+      (uint32_t)__builtin_amdgcn_readfirstlane((int)a.chunk_row0[chunk]);
+  const int nrows = __builtin_amdgcn_readfirstlane(a.chunk_rows[chunk]);
+  const int nb = (nrows + RB - 1) / RB;
+  const int nit = (nb + 1) / 2 + 1;  // iterations (the last only consumes)
+  const int sbytes = slot_bytes(p);
+  const int np = npieces(p);
+  const int xs_bytes = xspan(p);
+  double* bet = (double*)(smem + NSLOT * sbytes);  // [PMAX] theta of the partition
+  double* stdv = bet + PMAX;                        // [2][PMAX] center, 1/scale
+  int* ex = (int*)(stdv + 2 * PMAX);                // [PMAX] digit exponents E_f
+
+  for (int f = tid; f < PMAX; f += 64 * (NPW + NCW)) {
+    bet[f] = (f < P) ? a.theta[(int64_t)part * P + f] : 0.0;
+    ex[f] = digit_exponent(a.colmax[(int64_t)chunk * PMAX + f], FAM == FAMILY_LOGISTIC);
+    if constexpr (STD) {
+      const int j = f - ic;
+      const bool in = j >= 0 && j < p;
+      stdv[f] = in ? a.center[j] : 0.0;
+      stdv[PMAX + f] = in ? 1.0 / a.scale[j] : 1.0;
+    }
+  }
+  // (the ring needs no zeroing: past-the-chunk rows are zeroed in registers
+  // and nothing reads a slot's bytes that the DMA did not write)
+  __syncthreads();
+
+  auto slot_x = [&](int blk) -> char* {
+    const uintptr_t start = (uintptr_t)(a.X + (row0 + (int64_t)blk * RB) * p);
+    return smem + (blk % NSLOT) * sbytes + 16 + (start & 15);
+  };
+
+  if (wid >= NPW) {
+    // ======================= consumer waves ==================================
+    const int cw = wid - NPW;
+    const uintptr_t xcb = (uintptr_t)(a.X + row0 * p) & ~(uintptr_t)15;
+    const __amdgpu_buffer_rsrc_t xr = wv_rsrc(xcb, a.x_last16 + 16 - xcb);
+    const uintptr_t ycb = (uintptr_t)(a.y + row0);
+    const __amdgpu_buffer_rsrc_t yr = wv_rsrc(ycb, a.y_last4 + 4 - ycb);
+    // this wave's DMA pieces of a block: X pieces cw, cw + 4, ... (the last one
+    // only over its lanes inside the block), and (cw = 3) the block's y.
+    // Scalar bases per block; a piece is two scalar adds and the DMA.
+    const int npw = (np - cw + NCW - 1) / NCW;
+    const int per = npw + (cw == NCW - 1 ? 1 : 0);
+    const int last_rem = xs_bytes - (np - 1) * 1024;  // bytes of the last piece
+    // a block's slot LDS offset and the buffer offset of its 16-B-aligned start
+    auto blk_lds = [&](int blk) { return __builtin_amdgcn_readfirstlane((blk % NSLOT) * sbytes); };
+    auto blk_soff = [&](int blk) {
+      const uintptr_t start = (uintptr_t)(a.X + (row0 + (int64_t)blk * RB) * p);
+      return __builtin_amdgcn_readfirstlane((int)((start & ~(uintptr_t)15) - xcb));
+    };
+    auto issue_piece = [&](int blk, int lds, int soff, int i) {  // uniform: i < per
+      if (i < npw) {
+        const int j = cw + NCW * i;
+        if (j < np - 1 || lane * 16 < last_rem)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (wlds_void_t*)(smem + lds + 16 + j * 1024),
+                                                   16, lane * 16, soff + j * 1024, 0,
+                                                   DLSA_X_DMA_AUX);
+      } else {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(yr, (wlds_void_t*)(smem + lds + 16 + xs_bytes), 4,
+                                                 lane * 4, blk * RB * 8, 0, 0);
+      }
+    };
+    auto run = [&](auto cwI) {
+      constexpr int CW = decltype(cwI)::value;
+      if constexpr (DLSA_OZ_PRIO > 0) __builtin_amdgcn_s_setprio(DLSA_OZ_PRIO);
+      OzConsumer<NT, CW> C;
+      C.init();
+      for (int b = 0; b < 2 && b < nb; ++b) {
+        const int l0 = blk_lds(b), s0 = blk_soff(b);
+        for (int i = 0; i < per; ++i) issue_piece(b, l0, s0, i);
+      }
+      wv_wait_vmcnt<0>();
+      OZ_DECL;
+      for (int m = 0; m < nit; ++m) {
+        OZ_STAMP(t0);
+        barrier();  // B_m: blocks 2m, 2m+1 landed; the images of 2m-2, 2m-1 written
+        OZ_STAMP(t1);
+        // the DMA of blocks 2m+2, 2m+3 (into the slots of 2m-4, 2m-3), one piece
+        // after each tile's MFMAs, the rest after the tiles
+        const int nq = (2 * m + 2 < nb ? per : 0) + (2 * m + 3 < nb ? per : 0);
+        const int l0 = blk_lds(2 * m + 2), s0 = blk_soff(2 * m + 2);
+        const int l1 = blk_lds(2 * m + 3), s1 = blk_soff(2 * m + 3);
+        int q = 0;
+        auto tick = [&]() {
+          if (q < nq) {
+            if (q < per)
+              issue_piece(2 * m + 2, l0, s0, q);
+            else
+              issue_piece(2 * m + 3, l1, s1, q - per);
+            ++q;
+          }
+        };
+        if (!DLSA_OZ_TICK)  // (A/B: all of this iteration's DMA up front)
+          while (q < nq) tick();
+        if (m >= 1 && DLSA_OZ_ABLATE != 2) {
+          C.consume(slot_x(2 * m - 2), p, lane, tick);
+          if (2 * m - 1 < nb) C.consume(slot_x(2 * m - 1), p, lane, tick);
+        }
+        OZ_STAMP(t2);
+        while (q < nq) tick();
+        OZ_STAMP(t3);
+        wv_wait_vmcnt<0>();
+        OZ_STAMP(t4);
+        OZ_ADD(0, t1 - t0);
+        OZ_ADD(1, t3 - t2);
+        OZ_ADD(2, t2 - t1);
+        OZ_ADD(3, t4 - t3);
+      }
+      if (CW == 0) OZ_FLUSH(8);
+      __syncthreads();  // S1
+      C.store(a.slab_H + (int64_t)chunk * (NT * (NT + 1) / 2) * 256, ex, lane);
+      __syncthreads();  // S2 (the producers' reduction)
+    };
+    switch (cw) {
+      case 0: run(std::integral_constant<int, 0>{}); break;
+      case 1: run(std::integral_constant<int, 1>{}); break;
+      case 2: run(std::integral_constant<int, 2>{}); break;
+      default: run(std::integral_constant<int, 3>{}); break;
+    }
+    return;
+  }
+
+  // ========================= producer waves ==================================
+  const int pw = wid;
+  const int sl = lane / RPW;             // row phase: feature group
+  const int rr = lane % RPW;             // row of this wave's 8
+  const int rB = pw * RPW + rr;          // block row
+  const int k4 = rr >> 2;                // row quad of the wave's 8 rows
+  const uint32_t sel1 = (lane & 1) ? 0x03070105u : 0x06020400u;
+  const uint32_t sel2 = (lane & 2) ? 0x03020706u : 0x05040100u;
+  const int jq = lane & 3;               // lane in its quad: digit plane 4 - jq
+  double beta[M], gacc[M];
+  int esc[M];                            // 38 - E_f of this lane's features
+  uint32_t fmask = 0;                    // features f < P of this lane
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const int f = sl + LPR * m;
+    beta[m] = bet[f];
+    esc[m] = 38 - ex[f];
+    gacc[m] = 0.0;
+    if (f < P) fmask |= 1u << m;
+  }
+  double llacc = 0.0;
+
+  OZ_DECL;
+  for (int m = 0; m < nit; ++m) {
+    OZ_STAMP(t0);
+    barrier();  // B_m
+    OZ_STAMP(t1);
+    OZ_ADD(0, t1 - t0);
+    if (2 * m >= nb || DLSA_OZ_ABLATE == 1) continue;  // the last iteration only consumes
+    char* xsb[2];
+    const double* ysb[2];
+    int left[2];
+#pragma unroll
+    for (int X = 0; X < 2; ++X) {
+      const int b = 2 * m + X;  // b = nb (odd nb): all rows invalid, nothing consumed
+      xsb[X] = slot_x(b);
+      ysb[X] = (const double*)(smem + (b % NSLOT) * sbytes + 16 + xs_bytes);
+      left[X] = nrows - b * RB;
+    }
+    // ---- row phase of both blocks: 8 rows per wave, 8 lanes per row ---------
+    double xv[2][M], e[2], w[2], r[2];
+#pragma unroll
+    for (int X = 0; X < 2; ++X) {
+      const bool valid = rB < left[X];
+      const double* xr = (const double*)xsb[X] + rB * p + (sl - ic);
+      double e0 = 0.0, e1 = 0.0;
+#pragma unroll
+      for (int m2 = 0; m2 < M; ++m2) {
+        const int f = sl + LPR * m2;
+        double v = xr[LPR * m2];
+        if constexpr (STD) v = (v - stdv[f]) * stdv[PMAX + f];
+        if (m2 == 0 && ic && sl == 0) v = 1.0;
+        v = (valid && ((fmask >> m2) & 1u)) ? v : 0.0;
+        xv[X][m2] = v;
+        if (m2 & 1)
+          e1 = fma(v, beta[m2], e1);
+        else
+          e0 = fma(v, beta[m2], e0);
+      }
+      e[X] = e0 + e1;
+    }
+#pragma unroll
+    for (int X = 0; X < 2; ++X) e[X] = wv_row_sum<RPW>(e[X]);
+#pragma unroll
+    for (int X = 0; X < 2; ++X) {
+      const bool valid = rB < left[X];
+      const double yv = valid ? ysb[X][rB] : 0.0;
+      if constexpr (FAM == FAMILY_LOGISTIC) {
+        const double ea = exp(-fabs(e[X]));
+        const double inv = wv_rcp(1.0 + ea);
+        const double mu = e[X] >= 0.0 ? inv : ea * inv;
+        w[X] = ea * inv * inv;  // mu (1 - mu), cancellation free
+        r[X] = yv - mu;
+        if (valid && sl == 0) llacc += yv * e[X] - (fmax(e[X], 0.0) + wv_log12(1.0 + ea));
+      } else {  // gaussian (OLS): mu = eta, w = 1, ll = -rss / 2
+        w[X] = 1.0;
+        r[X] = yv - e[X];
+        if (valid && sl == 0) llacc -= 0.5 * r[X] * r[X];
+      }
+      if (!valid) {
+        w[X] = 0.0;
+        r[X] = 0.0;
+      }
+    }
+    OZ_STAMP(t2);
+    OZ_ADD(1, t2 - t1);
+    // ---- gradient and the digit images --------------------------------------
+#pragma unroll
+    for (int X = 0; X < 2; ++X) {
+      const double sw = FAM == FAMILY_LOGISTIC ? __builtin_sqrt(w[X]) : w[X];
+      // this wave's image over its own rows (read above): [feature][plane][8 rows]
+      char* img = xsb[X] + pw * RPW * p * 8 + k4 * 4;
+      uint32_t top[4];
+#pragma unroll
+      for (int m2 = 0; m2 < M; ++m2) {
+        gacc[m2] = fma(xv[X][m2], r[X], gacc[m2]);
+        const double t = fma(xv[X][m2], __builtin_amdgcn_ldexp(sw, esc[m2]), MAGIC);
+        const uint32_t lo = __double2loint(t);
+        // lane jq: byte jq of the quad's 4 rows = digit 4 - jq
+        const uint32_t dq = quad_transpose(lo, sel1, sel2) ^ 0x80808080u;
+        *(uint32_t*)(img + (sl + LPR * m2) * kFeatBytes + (4 - jq) * 8) = dq;
+        top[m2 & 3] = __double2hiint(t);
+        if ((m2 & 3) == 3 || m2 == M - 1) {  // digit 0 of up to 4 features
+          const int m0 = m2 & ~3, n = m2 - m0 + 1;
+#pragma unroll
+          for (int u = n; u < 4; ++u) top[u] = top[0];
+          const uint32_t t01 = perm(top[1], top[0], 0x05010400u);
+          const uint32_t t23 = perm(top[3], top[2], 0x05010400u);
+          const uint32_t tq = quad_transpose(perm(t23, t01, 0x05040100u), sel1, sel2) ^ 0x80808080u;
+          if (jq < n) *(uint32_t*)(img + (sl + LPR * (m0 + jq)) * kFeatBytes) = tq;
+        }
+      }
+    }
+#ifdef DLSA_OZ_PROF
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+    OZ_STAMP(t3);
+    OZ_ADD(2, t3 - t2);
+  }
+  if (pw == 0) OZ_FLUSH(0);
+  __syncthreads();  // S1 (the consumers' S1): the ring is free
+
+  // ---- epilogue: gradient and log-likelihood partials --------------------------
+  double* red = (double*)smem;  // the ring: [NPW][PMAX + 1]
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    double v = gacc[m];
+#pragma unroll
+    for (int o = 1; o < RPW; o <<= 1) v += __shfl_xor(v, o);
+    if (rr == 0) red[pw * (PMAX + 1) + sl + LPR * m] = v;
+  }
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) llacc += __shfl_xor(llacc, o);
+  if (lane == 0) red[pw * (PMAX + 1) + PMAX] = llacc;
+  __syncthreads();  // S2
+  for (int f = tid; f < PMAX; f += 64 * NPW) {
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < NPW; ++w) s += red[w * (PMAX + 1) + f];
+    a.slab_g[(int64_t)chunk * PMAX + f] = s;
+  }
+  if (tid == 0) {
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < NPW; ++w) s += red[w * (PMAX + 1) + PMAX];
+    a.slab_ll[chunk] = s;
+  }
+}
+
+template <int NT, bool STD, int FAM>
+static hipError_t launch_oz_t(const PassArgs& a, int n_chunks, hipStream_t s) {
+  auto kern = irls_oz_kernel<NT, STD, FAM>;
+  hipError_t e = ensure_max_lds((const void*)kern, 160 * 1024);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(kern, dim3(n_chunks), dim3(64 * (ozk::NPW + ozk::NCW)),
+                     ozk::lds_bytes(NT, a.p), s, a);
+  return hipGetLastError();
+}
+
+template <int NT>
+static hipError_t launch_oz_nt(const PassArgs& a, bool std_, int family, int n_chunks,
+                               hipStream_t s) {
+  if (family == FAMILY_GAUSSIAN)
+    return std_ ? launch_oz_t<NT, true, FAMILY_GAUSSIAN>(a, n_chunks, s)
+                : launch_oz_t<NT, false, FAMILY_GAUSSIAN>(a, n_chunks, s);
+  return std_ ? launch_oz_t<NT, true, FAMILY_LOGISTIC>(a, n_chunks, s)
+              : launch_oz_t<NT, false, FAMILY_LOGISTIC>(a, n_chunks, s);
+}
+
+}  // namespace dlsa

@@ -121,6 +121,8 @@ typedef struct dlsa_fit_stats {
                                escalated from bf16 (stall / lost definiteness) */
   int32_t polish_partitions; /* partitions left running by max_iter that got the
                                exact pass publishing Sig_inv at their theta */
+  int32_t passes_oz;        /* of passes_fp64: on the int8 matrix cores (Ozaki
+                               digit slices) */
 } dlsa_fit_stats;
 
 /* Default options (mixed Hessian, automatic chunking, no timing). */

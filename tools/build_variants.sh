@@ -21,9 +21,15 @@ for v in "$@"; do
     fab1) D=DLSA_FUSED_ABLATE=1 ;;
     wslot3) D=DLSA_WAVE_NSLOT=3 ;;
     word) D=DLSA_WAVE_ORDER=1 ;;
+    ozprof) D=DLSA_OZ_PROF=1 ;;
+    oz6) D=DLSA_OZ_LEVELS=6 ;;
+    oztick0) D=DLSA_OZ_TICK=0 ;;
+    ozprio0) D=DLSA_OZ_PRIO=0 ;;
+    ozab1) D="DLSA_OZ_ABLATE=1 -DDLSA_OZ_PROF=1" ;;
+    ozab2) D="DLSA_OZ_ABLATE=2 -DDLSA_OZ_PROF=1" ;;
     nt) D=DLSA_X_DMA_AUX=2 ;;
     sc1) D=DLSA_X_DMA_AUX=1 ;;
     *) echo "unknown variant $v"; exit 1 ;;
   esac
-  python -c "from dlsa_amd.build import build; print(build(force=True, out='tools/_variants/libdlsa_hip_$v.so', defines=['$D']))"
+  python -c "from dlsa_amd.build import build; print(build(force=True, out='tools/_variants/libdlsa_hip_$v.so', defines='$D'.replace('-D', '').split()))"
 done

@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--hessian", default="mixed")
     ap.add_argument("--rows-per-chunk", type=int, default=0)
     ap.add_argument("--warm", type=int, default=0, help="warm-start levels (0: full-row passes only)")
+    ap.add_argument("--max-iter", type=int, default=100)
     args = ap.parse_args()
 
     import numpy as np
@@ -95,7 +96,7 @@ def main():
                 opt.workspace_bytes = ws.numel()
                 rc = lib.dlsa_logistic_fit_batched_ex(
                     vp(X), vp(y), offs.ctypes.data_as(ctypes.c_void_p), K, p, 0, None, None,
-                    100, 1e-10, vp(theta), vp(sig), vp(sigt), vp(ll), vp(it), vp(st),
+                    args.max_iter, 1e-10, vp(theta), vp(sig), vp(sigt), vp(ll), vp(it), vp(st),
                     ctypes.byref(opt), stream)
                 if rc != 0:
                     raise RuntimeError(lib.dlsa_last_error().decode())
@@ -111,6 +112,21 @@ def main():
                 d["it"].append((s.passes_fp32, s.passes_fp64))
                 for kv in [x for x in kn.split(",") if x]:
                     os.environ.pop(kv.split("=")[0], None)
+                # profiling builds (DLSA_OZ_PROF): exact-pass stamp sums per 32-row block
+                prof = [0] * 16
+                for fn in ("dlsa_oz_prof_read", "dlsa_oz_prof_read_g2"):
+                    if hasattr(lib, fn):
+                        buf = (ctypes.c_ulonglong * 16)()
+                        getattr(lib, fn)(buf)
+                        prof = [a + b for a, b in zip(prof, buf)]
+                if any(prof):
+                    nit = max(1, n // 64 * max(1, s.passes_fp64))  # 64-row iterations
+                    d.setdefault("prof", []).append(
+                        {"producer": {k: round(prof[i] / nit, 1)
+                                      for i, k in enumerate(["barrier", "row", "digits"])},
+                         "consumer": {k: round(prof[8 + i] / nit, 1)
+                                      for i, k in enumerate(["barrier", "issue", "mfma",
+                                                             "vmwait"])}})
     for (name, kn), d in res.items():
         out = {"lib": name, "knobs": kn, "n": n, "p": p, "K": K, "passes": d["it"][-1]}
         for key in ("f32", "f64"):
@@ -120,6 +136,8 @@ def main():
                 out[f"{key}_GBps"] = round(bytes_per_pass / (m * 1e-3) / 1e9, 1)
         out["solve_ms_per_iter"] = round(statistics.median(d["solve"]), 3)
         out["fit_ms"] = round(statistics.median(d["total"]), 2)
+        if d.get("prof"):
+            out["cycles_per_block"] = d["prof"][-1]
         print(json.dumps(out), flush=True)
 
 
