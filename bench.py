@@ -422,7 +422,9 @@ def main():
         ms32, ms64 = tot("ms_pass_fp32"), tot("ms_pass_fp64")
         n32, n64 = tot("passes_fp32"), tot("passes_fp64")
         rows32, rows64 = tot("rows_fp32"), tot("rows_fp64")
-        exact = (f"irls_wave_kernel<NT={NT},fp64> (per-wave exact pass)" if NT <= 8
+        n_oz = tot("passes_oz")
+        exact = (f"irls_oz_kernel<NT={NT}> (exact pass, int8-MFMA digit slices)" if n_oz
+                 else f"irls_wave_kernel<NT={NT},fp64> (per-wave exact pass)" if NT <= 8
                  else f"irls_coop_kernel<NT={NT},fp64 Hessian>")
         if n32:
             kern["irls_coop<bf16 Hessian>"] = {
@@ -439,6 +441,9 @@ def main():
                 "mfma_TFps": rows64 * mfma_flops_per_row / (ms64 * 1e-3) / 1e12,
                 "mfma_frac": rows64 * mfma_flops_per_row / (ms64 * 1e-3) / 1e12
                 / FP64_MFMA_PEAK_TF}
+            if n_oz:  # the Hessian runs on the int8 matrix cores: bytes bound the pass
+                kern[exact]["note"] = ("X^T W X as int8 digit-slice products (DESIGN.md 4.1c); "
+                                       "mfma_* count the fp64-equivalent tile work")
         kern["newton_solve"] = {"ms_per_step": tot("ms_solve") / args.steps}
         if ms32 >= ms64:
             roof = hbm_roof(f"irls_coop_kernel<NT={NT},bf16 Hessian> (approximate-Hessian "

@@ -95,6 +95,7 @@ __host__ __device__ constexpr int slot_bytes(int p) { return 16 + xspan(p) + 256
 // planes + an unwritten sixth), so a lane's operand pair of planes (a, a+1),
 // a even, is one aligned 16-byte read
 constexpr int kFeatBytes = 48;
+constexpr int kMaxPiecesPerWave = 7;  // 1-KiB DMA pieces of a block per consumer wave
 // consumers issue the next blocks' DMA one piece per tile (1) or all before
 // their MFMAs (0)
 #ifndef DLSA_OZ_TICK
@@ -120,7 +121,8 @@ __host__ __device__ constexpr int lds_bytes(int NT, int p) {
 // the pass applies when a wave's image (+ skew) fits in the x bytes of its 8
 // rows and the ring fits the CU
 __host__ __device__ constexpr bool fits(int NT, int p) {
-  return img_bytes(NT) <= RPW * p * 8 && lds_bytes(NT, p) <= 160 * 1024;
+  return img_bytes(NT) <= RPW * p * 8 && lds_bytes(NT, p) <= 160 * 1024 &&
+         npieces(p) <= NCW * kMaxPiecesPerWave;
 }
 
 // Column strips J (tiles (I, J), I = J .. NT-1) dealt to the consumer waves,
@@ -330,7 +332,7 @@ struct OzConsumer {
           acc[t][6] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a4, Bq[2], acc[t][6], 0, 0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
-        tick();
+        tick(std::integral_constant<int, t>{});
       });
       // keep the level accumulators in registers across the loop
       wv_static_for<TW>([this](auto iI) {
@@ -417,9 +419,9 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
     const __amdgpu_buffer_rsrc_t yr = wv_rsrc(ycb, a.y_last4 + 4 - ycb);
     // this wave's DMA pieces of a block: X pieces cw, cw + 4, ... (the last one
     // only over its lanes inside the block), and (cw = 3) the block's y.
-    // Scalar bases per block; a piece is two scalar adds and the DMA.
+    // Scalar bases per block; piece i (a compile-time index) is two scalar
+    // adds and the DMA.
     const int npw = (np - cw + NCW - 1) / NCW;
-    const int per = npw + (cw == NCW - 1 ? 1 : 0);
     const int last_rem = xs_bytes - (np - 1) * 1024;  // bytes of the last piece
     // a block's slot LDS offset and the buffer offset of its 16-B-aligned start
     auto blk_lds = [&](int blk) { return __builtin_amdgcn_readfirstlane((blk % NSLOT) * sbytes); };
@@ -427,56 +429,71 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
       const uintptr_t start = (uintptr_t)(a.X + (row0 + (int64_t)blk * RB) * p);
       return __builtin_amdgcn_readfirstlane((int)((start & ~(uintptr_t)15) - xcb));
     };
-    auto issue_piece = [&](int blk, int lds, int soff, int i) {  // uniform: i < per
-      if (i < npw) {
+    auto issue_x = [&](auto iI, int lds, int soff) {
+      constexpr int i = decltype(iI)::value;
+      if (i < npw) {  // uniform
         const int j = cw + NCW * i;
-        if (j < np - 1 || lane * 16 < last_rem)
+        if (j != np - 1 || lane * 16 < last_rem)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (wlds_void_t*)(smem + lds + 16 + j * 1024),
                                                    16, lane * 16, soff + j * 1024, 0,
                                                    DLSA_X_DMA_AUX);
-      } else {
+      }
+    };
+    auto issue_y = [&](int blk, int lds) {
+      if (cw == NCW - 1)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(yr, (wlds_void_t*)(smem + lds + 16 + xs_bytes), 4,
                                                  lane * 4, blk * RB * 8, 0, 0);
-      }
+    };
+    // all of a block's pieces from piece I0 on
+    auto issue_rest = [&](auto I0, int blk, int lds, int soff) {
+      wv_static_for<kMaxPiecesPerWave>([&](auto iI) {
+        if constexpr (decltype(iI)::value >= decltype(I0)::value) issue_x(iI, lds, soff);
+      });
+      issue_y(blk, lds);
     };
     auto run = [&](auto cwI) {
       constexpr int CW = decltype(cwI)::value;
+      constexpr int TW = OzConsumer<NT, CW>::TW;
       if constexpr (DLSA_OZ_PRIO > 0) __builtin_amdgcn_s_setprio(DLSA_OZ_PRIO);
       OzConsumer<NT, CW> C;
       C.init();
-      for (int b = 0; b < 2 && b < nb; ++b) {
-        const int l0 = blk_lds(b), s0 = blk_soff(b);
-        for (int i = 0; i < per; ++i) issue_piece(b, l0, s0, i);
-      }
+      for (int b = 0; b < 2 && b < nb; ++b)
+        issue_rest(std::integral_constant<int, 0>{}, b, blk_lds(b), blk_soff(b));
       wv_wait_vmcnt<0>();
       OZ_DECL;
       for (int m = 0; m < nit; ++m) {
         OZ_STAMP(t0);
         barrier();  // B_m: blocks 2m, 2m+1 landed; the images of 2m-2, 2m-1 written
         OZ_STAMP(t1);
-        // the DMA of blocks 2m+2, 2m+3 (into the slots of 2m-4, 2m-3), one piece
-        // after each tile's MFMAs, the rest after the tiles
-        const int nq = (2 * m + 2 < nb ? per : 0) + (2 * m + 3 < nb ? per : 0);
+        // the DMA of blocks 2m+2, 2m+3 (into the slots of 2m-4, 2m-3): piece t
+        // of one block after tile t's MFMAs of each image, the rest after
+        const bool d0 = 2 * m + 2 < nb, d1 = 2 * m + 3 < nb;
         const int l0 = blk_lds(2 * m + 2), s0 = blk_soff(2 * m + 2);
         const int l1 = blk_lds(2 * m + 3), s1 = blk_soff(2 * m + 3);
-        int q = 0;
-        auto tick = [&]() {
-          if (q < nq) {
-            if (q < per)
-              issue_piece(2 * m + 2, l0, s0, q);
-            else
-              issue_piece(2 * m + 3, l1, s1, q - per);
-            ++q;
-          }
+        auto tick0 = [&](auto tI) {
+          if (DLSA_OZ_TICK && d0) issue_x(tI, l0, s0);
         };
-        if (!DLSA_OZ_TICK)  // (A/B: all of this iteration's DMA up front)
-          while (q < nq) tick();
-        if (m >= 1 && DLSA_OZ_ABLATE != 2) {
-          C.consume(slot_x(2 * m - 2), p, lane, tick);
-          if (2 * m - 1 < nb) C.consume(slot_x(2 * m - 1), p, lane, tick);
-        }
+        auto tick1 = [&](auto tI) {
+          if (DLSA_OZ_TICK && d1) issue_x(tI, l1, s1);
+        };
+        constexpr int I0 = DLSA_OZ_TICK ? TW : 0;
+        const bool c1 = m >= 1 && 2 * m - 1 < nb && DLSA_OZ_ABLATE != 2;
+        if (m >= 1 && DLSA_OZ_ABLATE != 2) C.consume(slot_x(2 * m - 2), p, lane, tick0);
+        if (c1) C.consume(slot_x(2 * m - 1), p, lane, tick1);
         OZ_STAMP(t2);
-        while (q < nq) tick();
+        // pieces not yet issued: all of a block whose image tick did not run
+        if (d0) {
+          if (m >= 1 && DLSA_OZ_ABLATE != 2)
+            issue_rest(std::integral_constant<int, I0>{}, 2 * m + 2, l0, s0);
+          else
+            issue_rest(std::integral_constant<int, 0>{}, 2 * m + 2, l0, s0);
+        }
+        if (d1) {
+          if (c1)
+            issue_rest(std::integral_constant<int, I0>{}, 2 * m + 3, l1, s1);
+          else
+            issue_rest(std::integral_constant<int, 0>{}, 2 * m + 3, l1, s1);
+        }
         OZ_STAMP(t3);
         wv_wait_vmcnt<0>();
         OZ_STAMP(t4);
@@ -562,40 +579,55 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
     }
 #pragma unroll
     for (int X = 0; X < 2; ++X) e[X] = wv_row_sum<RPW>(e[X]);
-#pragma unroll
-    for (int X = 0; X < 2; ++X) {
-      const bool valid = rB < left[X];
-      const double yv = valid ? ysb[X][rB] : 0.0;
+    // One transcendental chain for the 16 rows of both blocks: lanes 0-31 take
+    // block 0's row rr (lane % 8), lanes 32-63 block 1's (every lane of a row
+    // holds its eta), then each lane fetches the other block's results from
+    // lane ^ 32 (the same row rr): half the chain instructions of one chain
+    // per block.
+    const bool hb = lane >= 32;
+    double sw[2];
+    {
+      const double eh = hb ? e[1] : e[0];
+      const int lh = hb ? left[1] : left[0];
+      const bool valid = rB < lh;
+      const double yv = valid ? ysb[hb ? 1 : 0][rB] : 0.0;
+      double wh, rh;
       if constexpr (FAM == FAMILY_LOGISTIC) {
-        const double ea = exp(-fabs(e[X]));
+        const double ea = exp(-fabs(eh));
         const double inv = wv_rcp(1.0 + ea);
-        const double mu = e[X] >= 0.0 ? inv : ea * inv;
-        w[X] = ea * inv * inv;  // mu (1 - mu), cancellation free
-        r[X] = yv - mu;
-        if (valid && sl == 0) llacc += yv * e[X] - (fmax(e[X], 0.0) + wv_log12(1.0 + ea));
+        const double mu = eh >= 0.0 ? inv : ea * inv;
+        wh = ea * inv * inv;  // mu (1 - mu), cancellation free
+        rh = yv - mu;
+        if (valid && (sl & 3) == 0) llacc += yv * eh - (fmax(eh, 0.0) + wv_log12(1.0 + ea));
       } else {  // gaussian (OLS): mu = eta, w = 1, ll = -rss / 2
-        w[X] = 1.0;
-        r[X] = yv - e[X];
-        if (valid && sl == 0) llacc -= 0.5 * r[X] * r[X];
+        wh = 1.0;
+        rh = yv - eh;
+        if (valid && (sl & 3) == 0) llacc -= 0.5 * rh * rh;
       }
       if (!valid) {
-        w[X] = 0.0;
-        r[X] = 0.0;
+        wh = 0.0;
+        rh = 0.0;
       }
+      const double swh = FAM == FAMILY_LOGISTIC ? __builtin_sqrt(wh) : wh;
+      const double swo = wv_swap32(swh, hb), ro = wv_swap32(rh, hb);
+      sw[0] = hb ? swo : swh;
+      sw[1] = hb ? swh : swo;
+      r[0] = hb ? ro : rh;
+      r[1] = hb ? rh : ro;
     }
+    (void)w;
     OZ_STAMP(t2);
     OZ_ADD(1, t2 - t1);
     // ---- gradient and the digit images --------------------------------------
 #pragma unroll
     for (int X = 0; X < 2; ++X) {
-      const double sw = FAM == FAMILY_LOGISTIC ? __builtin_sqrt(w[X]) : w[X];
       // this wave's image over its own rows (read above): [feature][plane][8 rows]
       char* img = xsb[X] + pw * RPW * p * 8 + k4 * 4;
       uint32_t top[4];
 #pragma unroll
       for (int m2 = 0; m2 < M; ++m2) {
         gacc[m2] = fma(xv[X][m2], r[X], gacc[m2]);
-        const double t = fma(xv[X][m2], __builtin_amdgcn_ldexp(sw, esc[m2]), MAGIC);
+        const double t = fma(xv[X][m2], __builtin_amdgcn_ldexp(sw[X], esc[m2]), MAGIC);
         const uint32_t lo = __double2loint(t);
         // lane jq: byte jq of the quad's 4 rows = digit 4 - jq
         const uint32_t dq = quad_transpose(lo, sel1, sel2) ^ 0x80808080u;

@@ -76,6 +76,15 @@ __device__ __forceinline__ double wv_xor32(double v) {
   const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
   return __hiloint2double(b[0], a[0]) + __hiloint2double(b[1], a[1]);
 }
+// The value of lane l ^ 32.  v_permlane32_swap exchanges lanes 32-63 of vdst
+// with lanes 0-31 of src: with both = v, vdst holds the partner's value in
+// the upper half and src in the lower half.
+__device__ __forceinline__ double wv_swap32(double v, bool upper) {
+  const unsigned lo = __double2loint(v), hi = __double2hiint(v);
+  const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  return upper ? __hiloint2double(b[0], a[0]) : __hiloint2double(b[1], a[1]);
+}
 template <int CTRL>
 __device__ __forceinline__ double wv_dpp(double v) {
   const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
