@@ -319,9 +319,14 @@ void irls_coop_kernel(const PassArgs a) {
 #pragma unroll
   for (int m = 0; m < M; ++m) asm volatile("" : "+v"(beta[m]));
   double llacc = 0.0;
-  uint32_t cmx[CM ? M : 1];  // CM: running max of |x| high dwords per feature
+  // CM: running max of |x| per feature.  One v_max_f64 with the abs modifier
+  // per value and no row mask: the rows of a chunk's last block past its end
+  // are the next chunk's rows (or the range check's zeros), so the recorded
+  // max is an upper bound over the chunk's rows, which is all the digit
+  // exponents need (a looser bound only moves the digits down a bit).
+  double cmx[CM ? M : 1];
 #pragma unroll
-  for (int m = 0; m < (CM ? M : 1); ++m) cmx[m] = 0u;
+  for (int m = 0; m < (CM ? M : 1); ++m) cmx[m] = 0.0;
   int tI[G::TPW], tJ[G::TPW];  // this wave's tiles (bf16 path)
 #pragma unroll
   for (int i = 0; i < G::TPW; ++i) {
@@ -400,7 +405,7 @@ void irls_coop_kernel(const PassArgs a) {
         if constexpr (STD) v = (v - stdv[sl + LPR * m]) * stdv[G::PMAX + sl + LPR * m];
         if (m == 0 && ic && sl == 0) v = 1.0;
         xv[m] = v;
-        if constexpr (CM) cmx[m] = max(cmx[m], valid ? (__double2hiint(v) & 0x7FFFFFFFu) : 0u);
+        if constexpr (CM) asm("v_max_f64 %0, %0, |%1|" : "+v"(cmx[m]) : "v"(v));
         if (m & 1)
           e1 = fma(v, beta[m], e1);
         else
@@ -523,7 +528,7 @@ void irls_coop_kernel(const PassArgs a) {
     uint32_t* cred = (uint32_t*)smem;  // [W][PMAX]
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-      uint32_t v = cmx[m];
+      uint32_t v = __double2hiint(cmx[m]) & 0x7FFFFFFFu;
 #pragma unroll
       for (int o = 1; o < RPW; o <<= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
       if (lane % RPW == 0) cred[wid * G::PMAX + sl + LPR * m] = v;

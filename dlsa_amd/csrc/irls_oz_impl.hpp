@@ -24,8 +24,9 @@
 // keeping the levels k < NL: H_ij = 2^(E_i + E_j - 12) sum_{k<NL} 2^(-8k) L_k.
 // The integer sums are exact and order-free; the error is the rounding of z
 // to 38 bits below 2^E_f and the dropped levels (~2^(-8 NL) of a row's leading
-// product, random in sign): ~1e-11 relative at NL = 5 (profiles/r03i), within
-// the path's 1e-8 tolerance by three orders (tests/test_gpu_parity.py).
+// product, random in sign): 2.15e-12 against the oracle at config 2, as the
+// fp64 pass (profiles/r03w_bench_c2.json), and within 1e-11 of the fp64 pass at
+// the same iterate (tests/test_gpu_ozaki.py).
 //
 // MFMA pairing.  One v_mfma_i32_16x16x64_i8 sums 64 k slots; a 32-row block
 // fills them with TWO digit products: lane group g holds the 8 rows of
