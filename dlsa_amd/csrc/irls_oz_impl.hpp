@@ -537,7 +537,7 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
     gacc[m] = 0.0;
     if (f < P) fmask |= 1u << m;
   }
-  double llacc = 0.0;
+  double llacc = 0.0, lprod = 1.0;
 
   OZ_DECL;
   for (int m = 0; m < nit; ++m) {
@@ -557,7 +557,7 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
       left[X] = nrows - b * RB;
     }
     // ---- row phase of both blocks: 8 rows per wave, 8 lanes per row ---------
-    double xv[2][M], e[2], w[2], r[2];
+    double xv[2][M], e[2], r[2];
 #pragma unroll
     for (int X = 0; X < 2; ++X) {
       const bool valid = rB < left[X];
@@ -592,31 +592,37 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
       const int lh = hb ? left[1] : left[0];
       const bool valid = rB < lh;
       const double yv = valid ? ysb[hb ? 1 : 0][rB] : 0.0;
-      double wh, rh;
+        // sqrt(w) = sqrt(e^-|eta|) / (1 + e^-|eta|): one exp of -|eta|/2 gives
+      // both (no sqrt); the softplus log(1 + e^-|eta|) of the log-likelihood
+      // goes into a running product per lane, one log at the end (a chunk is
+      // <= 512 iterations, so the product of terms in [1, 2] stays < 2^512)
+      double swh, rh;
       if constexpr (FAM == FAMILY_LOGISTIC) {
-        const double ea = exp(-fabs(eh));
+        const double eq = exp(-0.5 * fabs(eh));
+        const double ea = eq * eq;
         const double inv = wv_rcp(1.0 + ea);
         const double mu = eh >= 0.0 ? inv : ea * inv;
-        wh = ea * inv * inv;  // mu (1 - mu), cancellation free
+        swh = eq * inv;
         rh = yv - mu;
-        if (valid && (sl & 3) == 0) llacc += yv * eh - (fmax(eh, 0.0) + wv_log12(1.0 + ea));
+        if (valid && (sl & 3) == 0) {
+          llacc += yv * eh - fmax(eh, 0.0);
+          lprod *= 1.0 + ea;
+        }
       } else {  // gaussian (OLS): mu = eta, w = 1, ll = -rss / 2
-        wh = 1.0;
+        swh = 1.0;
         rh = yv - eh;
         if (valid && (sl & 3) == 0) llacc -= 0.5 * rh * rh;
       }
       if (!valid) {
-        wh = 0.0;
+        swh = 0.0;
         rh = 0.0;
       }
-      const double swh = FAM == FAMILY_LOGISTIC ? __builtin_sqrt(wh) : wh;
       const double swo = wv_swap32(swh, hb), ro = wv_swap32(rh, hb);
       sw[0] = hb ? swo : swh;
       sw[1] = hb ? swh : swo;
       r[0] = hb ? ro : rh;
       r[1] = hb ? rh : ro;
     }
-    (void)w;
     OZ_STAMP(t2);
     OZ_ADD(1, t2 - t1);
     // ---- gradient and the digit images --------------------------------------
@@ -663,6 +669,7 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
     for (int o = 1; o < RPW; o <<= 1) v += __shfl_xor(v, o);
     if (rr == 0) red[pw * (PMAX + 1) + sl + LPR * m] = v;
   }
+  if constexpr (FAM == FAMILY_LOGISTIC) llacc -= log(lprod);
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) llacc += __shfl_xor(llacc, o);
   if (lane == 0) red[pw * (PMAX + 1) + PMAX] = llacc;
