@@ -592,7 +592,7 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
       const int lh = hb ? left[1] : left[0];
       const bool valid = rB < lh;
       const double yv = valid ? ysb[hb ? 1 : 0][rB] : 0.0;
-        // sqrt(w) = sqrt(e^-|eta|) / (1 + e^-|eta|): one exp of -|eta|/2 gives
+      // sqrt(w) = sqrt(e^-|eta|) / (1 + e^-|eta|): one exp of -|eta|/2 gives
       // both (no sqrt); the softplus log(1 + e^-|eta|) of the log-likelihood
       // goes into a running product per lane, one log at the end (a chunk is
       // <= 512 iterations, so the product of terms in [1, 2] stays < 2^512)
