@@ -108,7 +108,7 @@ constexpr int kMaxPiecesPerWave = 7;  // 1-KiB DMA pieces of a block per consume
 #ifndef DLSA_OZ_PRIO
 #define DLSA_OZ_PRIO 1
 #endif
-// profiling-only ablations: 1 producers skip the row phase and digits, 2
+// profiling-only ablations (bits): 1 producers skip the row phase and digits, 2
 // consumers skip the MFMAs
 #ifndef DLSA_OZ_ABLATE
 #define DLSA_OZ_ABLATE 0
@@ -478,13 +478,13 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
           if (DLSA_OZ_TICK && d1) issue_x(tI, l1, s1);
         };
         constexpr int I0 = DLSA_OZ_TICK ? TW : 0;
-        const bool c1 = m >= 1 && 2 * m - 1 < nb && DLSA_OZ_ABLATE != 2;
-        if (m >= 1 && DLSA_OZ_ABLATE != 2) C.consume(slot_x(2 * m - 2), p, lane, tick0);
+        const bool c1 = m >= 1 && 2 * m - 1 < nb && !(DLSA_OZ_ABLATE & 2);
+        if (m >= 1 && !(DLSA_OZ_ABLATE & 2)) C.consume(slot_x(2 * m - 2), p, lane, tick0);
         if (c1) C.consume(slot_x(2 * m - 1), p, lane, tick1);
         OZ_STAMP(t2);
         // pieces not yet issued: all of a block whose image tick did not run
         if (d0) {
-          if (m >= 1 && DLSA_OZ_ABLATE != 2)
+          if (m >= 1 && !(DLSA_OZ_ABLATE & 2))
             issue_rest(std::integral_constant<int, I0>{}, 2 * m + 2, l0, s0);
           else
             issue_rest(std::integral_constant<int, 0>{}, 2 * m + 2, l0, s0);
@@ -545,7 +545,7 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
     barrier();  // B_m
     OZ_STAMP(t1);
     OZ_ADD(0, t1 - t0);
-    if (2 * m >= nb || DLSA_OZ_ABLATE == 1) continue;  // the last iteration only consumes
+    if (2 * m >= nb || (DLSA_OZ_ABLATE & 1)) continue;  // the last iteration only consumes
     char* xsb[2];
     const double* ysb[2];
     int left[2];

@@ -27,6 +27,7 @@ for v in "$@"; do
     ozprio0) D=DLSA_OZ_PRIO=0 ;;
     ozab1) D="DLSA_OZ_ABLATE=1 -DDLSA_OZ_PROF=1" ;;
     ozab2) D="DLSA_OZ_ABLATE=2 -DDLSA_OZ_PROF=1" ;;
+    ozab3) D="DLSA_OZ_ABLATE=3 -DDLSA_OZ_PROF=1" ;;
     nt) D=DLSA_X_DMA_AUX=2 ;;
     sc1) D=DLSA_X_DMA_AUX=1 ;;
     *) echo "unknown variant $v"; exit 1 ;;
