@@ -10,7 +10,6 @@ for v in "$@"; do
     ablate2) D=DLSA_ABLATE=2 ;;
     ablate3) D=DLSA_ABLATE=3 ;;
     ablate4) D=DLSA_ABLATE=4 ;;
-    catk) D=DLSA_CAT_KARG=1 ;;
     cat1) D=DLSA_CAT_ABLATE=1 ;;
     cat2) D=DLSA_CAT_ABLATE=2 ;;
     cat4) D=DLSA_CAT_ABLATE=4 ;;
