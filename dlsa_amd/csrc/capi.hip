@@ -142,6 +142,22 @@ static int32_t* pinned_staging(size_t n_i32) {
   return buf;
 }
 
+// Device buffer of the wide path's int8 digit records (wide_oz.hip), grown on
+// demand and kept for the process (several GB at config 5: no allocation and
+// mapping per fit).
+static int8_t* digit_buffer(size_t bytes) {
+  static int8_t* buf = nullptr;
+  static size_t cap = 0;
+  if (cap < bytes) {
+    if (buf) (void)hipFree(buf);
+    buf = nullptr;
+    cap = 0;
+    if (hipMalloc((void**)&buf, bytes) != hipSuccess) return nullptr;
+    cap = bytes;
+  }
+  return buf;
+}
+
 static double warm_level_tol(bool fused) {
   if (const char* e = getenv("DLSA_LEVEL_TOL")) return atof(e);
   return fused ? 0.2 : 0.1;
@@ -265,6 +281,7 @@ struct WideLayout {
   int64_t off_offsets, off_w, off_slabg, off_slabll, off_slabG, off_slabgz, off_slabllz, off_H;
   int64_t off_phase, off_bt, off_llprev, off_thprev, off_dprev, off_counters;
   int64_t off_dmprev, off_stall;
+  int64_t off_zmax, off_ozE;  // int8 exact Gram: row-chunk max |z|, digit exponents
   int64_t total;
   int64_t cap_rows, cap_gram;  // row-chunk / Gram-row-group capacity of the tables and slabs
 };
@@ -314,6 +331,8 @@ static WideLayout make_wide_layout(const std::vector<WidePlans>& plans, int K, i
   L.off_counters = take(16);
   L.off_dmprev = take(8LL * K);
   L.off_stall = take(4LL * K);
+  L.off_zmax = take(4 * nr * PP);
+  L.off_ozE = take(4LL * K * PP);
   L.total = o;
   L.cap_rows = nr;
   L.cap_gram = ng;
@@ -636,6 +655,56 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
   }
   int32_t* h_phase = h_cnt + 4;  // [K] phases (pinned: no staging copy per iteration)
 
+  // The exact Gram pass: on the int8 matrix cores (wide_oz.hip) in mixed mode
+  // when every Gram row group of the final plan is <= 32767 rows and the digit
+  // records fit their budget (DLSA_OZ=0: always the fp64 Gram).  The row pass
+  // then also records each chunk's max |sqrt(w) x|, from which the scale kernel
+  // takes the digit exponents.
+  const Plan& fg = plans.back().gram;
+  int max_grows = 0;
+  for (int c = 0; c < fg.n_chunks; ++c) max_grows = std::max(max_grows, fg.chunk_rows[c]);
+  WideOzArgs woz;
+  memset(&woz, 0, sizeof(woz));
+  woz.rcb = d_rcb;
+  woz.zmax = (const uint32_t*)at(L.off_zmax);
+  woz.E = (int32_t*)at(L.off_ozE);
+  woz.maxblk = (max_grows + 31) / 32;
+  const int PPw = kWideTile * NB;
+  const size_t digit_bytes = (size_t)std::max(fg.n_chunks, 1) * woz.maxblk * 4 * PPw * 48;
+  const bool use_wide_oz = !(getenv("DLSA_OZ") && atoi(getenv("DLSA_OZ")) == 0) &&
+                           family == FAMILY_LOGISTIC && opt.hessian_mode == DLSA_HESSIAN_MIXED &&
+                           max_grows <= kWideOzMaxRows && digit_bytes <= (size_t(32) << 30);
+  if (use_wide_oz) {
+    woz.D = digit_buffer(digit_bytes);
+    if (!woz.D) {
+      set_error("digit buffer allocation failed");
+      return DLSA_E_HIP;
+    }
+  }
+  auto exact_gram = [&](const WidePlans& q, bool final_level) -> hipError_t {
+    const bool oz = use_wide_oz && final_level;
+    wa.slab_zmax = oz ? (uint32_t*)at(L.off_zmax) : nullptr;
+    hipError_t e = timed(&g_stats.ms_wide_row, [&] {
+      return launch_wide_row(wa, standardize, family, q.rows.n_chunks, stream);
+    });
+    wa.slab_zmax = nullptr;
+    if (e != hipSuccess) return e;
+    if (!oz)
+      return timed(
+          &g_stats.ms_wide_gram, [&] { return launch_wide_gram(wa, standardize, stream); },
+          &g_stats.ms_pass_fp64);
+    g_stats.passes_oz++;
+    return timed(
+        &g_stats.ms_wide_gram,
+        [&] {
+          hipError_t e2 = launch_wide_oz_scale(wa, woz, K, stream);
+          if (e2 == hipSuccess) e2 = launch_wide_oz_digits(wa, woz, standardize, stream);
+          if (e2 == hipSuccess) e2 = launch_wide_oz_gram(wa, woz, stream);
+          return e2;
+        },
+        &g_stats.ms_pass_fp64);
+  };
+
   int it = 0;
   for (size_t lvl = 0; lvl < plans.size(); ++lvl) {
     const WidePlans& q = plans[lvl];
@@ -674,14 +743,9 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
         g_stats.passes_fp32++;
         g_stats.rows_fp32 += phase_rows(part_rows, h_phase, PHASE_F32);
       }
-      // exact partitions: row pass (gradient, w) + fp64 Gram pass
+      // exact partitions: row pass (gradient, w) + the exact Gram pass
       if (n_running[PHASE_F64] > 0) {
-        DLSA_HIP_TRY(timed(&g_stats.ms_wide_row, [&] {
-          return launch_wide_row(wa, standardize, family, q.rows.n_chunks, stream);
-        }));
-        DLSA_HIP_TRY(timed(
-            &g_stats.ms_wide_gram, [&] { return launch_wide_gram(wa, standardize, stream); },
-            &g_stats.ms_pass_fp64));
+        DLSA_HIP_TRY(exact_gram(q, final_level));
         g_stats.passes_fp64++;
         g_stats.rows_fp64 += phase_rows(part_rows, h_phase, PHASE_F64);
       }
@@ -708,12 +772,7 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
     DLSA_HIP_TRY(hipMemcpyAsync(h_phase, d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
     DLSA_HIP_TRY(hipStreamSynchronize(stream));
     const std::vector<int64_t> part_rows = plan_part_rows(q.rows, K);
-    DLSA_HIP_TRY(timed(&g_stats.ms_wide_row, [&] {
-      return launch_wide_row(wa, standardize, family, q.rows.n_chunks, stream);
-    }));
-    DLSA_HIP_TRY(timed(
-        &g_stats.ms_wide_gram, [&] { return launch_wide_gram(wa, standardize, stream); },
-        &g_stats.ms_pass_fp64));
+    DLSA_HIP_TRY(exact_gram(q, true));
     g_stats.passes_fp64++;
     g_stats.rows_fp64 += phase_rows(part_rows, h_phase, PHASE_F64);
     g_stats.polish_partitions = running_total(n_running);

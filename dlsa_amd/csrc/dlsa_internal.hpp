@@ -187,7 +187,24 @@ struct WideArgs {
   int32_t p, P, intercept;
   int32_t NB;              // 128-wide column blocks, PP = 128 NB
   int32_t n_gchunks;
+  // int8 exact Gram (wide_oz.hip): the row pass's per-chunk max |sqrt(w) x|
+  // (high dwords, [n_rchunks, PP]) when set
+  uint32_t* slab_zmax;
 };
+
+// int8 exact Gram of the wide path (wide_oz.hip)
+struct WideOzArgs {
+  const int32_t* rcb;      // [K+1] row-pass chunks of each partition
+  const uint32_t* zmax;    // [n_rchunks, PP] the row pass's max |sqrt(w) x| high dwords
+  int32_t* E;              // [K, PP] digit exponents
+  int8_t* D;               // digit records [n_gchunks][maxblk][4][PP][48]
+  int32_t maxblk;          // 32-row blocks of the largest Gram row group
+};
+hipError_t launch_wide_oz_scale(const WideArgs& a, const WideOzArgs& o, int K, hipStream_t s);
+hipError_t launch_wide_oz_digits(const WideArgs& a, const WideOzArgs& o, bool standardize,
+                                 hipStream_t s);
+hipError_t launch_wide_oz_gram(const WideArgs& a, const WideOzArgs& o, hipStream_t s);
+constexpr int kWideOzMaxRows = 32767;  // int32 level sums of one row group
 
 // Categorical-code pass (cat_pass.hip): q numeric fp64 columns + F uint8
 // level codes per row; the one-hot blocks of X^T W X are LDS histograms.

@@ -110,6 +110,11 @@ __global__ __launch_bounds__(256) void wide_row_kernel(const WideArgs a) {
   }
   const bool icpt_lane = ic && lane == 0;
   double llacc = 0.0;
+  // int8 exact Gram: running max of |sqrt(w) x| high dwords per feature
+  const bool zm_on = a.slab_zmax != nullptr;
+  uint32_t zmx[MB];
+#pragma unroll
+  for (int m = 0; m < MB; ++m) zmx[m] = 0u;
   constexpr int U = 4;  // rows per wave per step (all U rows' loads in flight)
   for (int base = wid * U; base < nrows; base += 4 * U) {
     double xv[U][MB], yv[U];
@@ -150,6 +155,12 @@ __global__ __launch_bounds__(256) void wide_row_kernel(const WideArgs a) {
       if (!valid) r = 0.0;
 #pragma unroll
       for (int m = 0; m < MB; ++m) gacc[m] = fma(xv[u][m], r, gacc[m]);
+      if (zm_on) {
+        const double sw = valid ? sqrt(w) : 0.0;
+#pragma unroll
+        for (int m = 0; m < MB; ++m)
+          zmx[m] = max(zmx[m], (uint32_t)__double2hiint(xv[u][m] * sw) & 0x7FFFFFFFu);
+      }
       if (valid && lane == 0) a.w[row0 + base + u] = w;
     }
   }
@@ -164,6 +175,15 @@ __global__ __launch_bounds__(256) void wide_row_kernel(const WideArgs a) {
         ((red[f] + red[PP + f]) + red[2 * PP + f]) + red[3 * PP + f];
   if (tid == 0)
     a.slab_ll[chunk] = ((red[4 * PP] + red[4 * PP + 1]) + red[4 * PP + 2]) + red[4 * PP + 3];
+  if (zm_on) {
+    __shared__ uint32_t zred[4 * 64 * MB];
+#pragma unroll
+    for (int m = 0; m < MB; ++m) zred[wid * 64 * MB + lane + 64 * m] = zmx[m];
+    __syncthreads();
+    for (int f = tid; f < PP; f += 256)
+      a.slab_zmax[(int64_t)chunk * PP + f] =
+          max(max(zred[f], zred[PP + f]), max(zred[2 * PP + f], zred[3 * PP + f]));
+  }
 }
 
 // ---------------------------------------------------------------------------

@@ -134,3 +134,30 @@ def test_ozaki_fallbacks_keep_the_fp64_pass(torch_cuda, M, case):
     th, S, _, _, _ = O.logistic_fit_partitions(X, y, off)
     assert _rel(fit.theta.cpu(), th) < REL
     assert _rel(fit.sig_inv.cpu(), S) < REL
+
+
+@pytest.mark.parametrize("p,fi,std", [(200, True, False), (300, False, True), (500, True, False)])
+def test_wide_ozaki_gram_matches_fp64_gram(torch_cuda, M, monkeypatch, p, fi, std):
+    """Wide path (P > 192, wide_oz.hip): the exact Gram from int8 digit records
+    (exponents from the row pass's max |sqrt(w) x| per partition) against the
+    fp64 Gram at the same iterate, and the fit against the oracle."""
+    sizes = [6000, 5001]
+    n = sum(sizes)
+    X, y = O.simulate_counter(n, p, seed=13 * p + fi)
+    center = scale = None
+    if std:
+        X = X * 3.0 - 0.7
+        center, scale = X.mean(0), X.std(0)
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    oz, f64 = _pair(M, monkeypatch, X, y, off, fit_intercept=fi, center=center, scale=scale,
+                    rows_per_chunk=2000)
+    assert oz.stats["passes_oz"] >= 1 and f64.stats["passes_oz"] == 0
+    assert (oz.status.cpu().numpy() == 0).all()
+    assert _rel(oz.sig_inv.cpu(), f64.sig_inv.cpu()) < OZ_REL
+    assert _rel(oz.theta.cpu(), f64.theta.cpu()) < 1e-12
+    assert _rel(oz.loglik.cpu(), f64.loglik.cpu()) < 1e-12
+    th, S, St, ll, _ = O.logistic_fit_partitions(X, y, off, fit_intercept=fi, center=center,
+                                                 scale=scale)
+    assert _rel(oz.theta.cpu(), th) < REL
+    assert _rel(oz.sig_inv.cpu(), S) < REL
+    assert _rel(oz.sig_inv_theta.cpu(), St) < REL
