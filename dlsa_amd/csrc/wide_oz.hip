@@ -11,9 +11,11 @@
 //   wide_oz_scale_kernel per partition and feature E_f with |z| < 2^E_f
 //   wide_oz_digits_kernel  F = round(z 2^(38 - E_f)) by one FMA against
 //                        1.5 2^52 + 0x8080808080; its five bytes XOR 0x80 are
-//                        balanced digits d_0 .. d_4, written as records of
-//                        48 bytes per (8 rows, feature): byte 8 d + r = digit d
-//                        of row r (the layout irls_oz_impl.hpp's consumers read)
+//                        balanced digits d_0 .. d_4 (byte r of plane d = digit
+//                        d of row r), stored per 8 rows as three slices of
+//                        [feature][16 B] (planes 0-1, 2-3, 4): a wave's store
+//                        of a slice is 1 KB contiguous, and the consumers'
+//                        fragment reads are 16-byte strided (no bank conflicts)
 //   wide_oz_gram_kernel  per (row group, 128 x 128 tile): 8 waves, each a
 //                        64 x 32 block (4 x 2 sub-tiles of 16 x 16), NL = 5
 //                        int32 level accumulators per sub-tile; per 32-row step
@@ -112,10 +114,10 @@ __global__ __launch_bounds__(256) void wide_oz_digits_kernel(const WideArgs a, c
     q2.y = pack(lo, 0, 4);
     q2.z = 0u;
     q2.w = 0u;
-    uint4* dst = (uint4*)(rec + (int64_t)f * kRec);
+    uint4* dst = (uint4*)(rec + (int64_t)f * 16);
     dst[0] = q0;
-    dst[1] = q1;
-    dst[2] = q2;
+    dst[PP] = q1;
+    dst[2 * PP] = q2;
   }
 }
 
@@ -155,10 +157,11 @@ __global__ __launch_bounds__(512, 1) void wide_oz_gram_kernel(const WideArgs a, 
     for (int i = 0; i < 6; ++i) {
       const int pc = wid * 6 + i;        // 0 .. 47
       const int ab = pc / 24, q = pc % 24;  // panel, piece within it
-      const int j = q / 6, k = q % 6;     // rowblock, 1 KB of its 6 KB
-      const int soff = s * stepb + j * PP * kRec + (ab ? J : I) * kOzGT * kRec + k * 1024;
+      const int j = q / 6, sl = (q % 6) >> 1, k = q & 1;  // rowblock, slice, 1 KB half
+      const int soff = s * stepb + j * PP * kRec + sl * PP * 16 + (ab ? J : I) * kOzGT * 16 + k * 1024;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          dr, (wlds_void_t*)(st + ab * kPanel + j * kOzGT * kRec + k * 1024), 16, lane * 16,
+          dr, (wlds_void_t*)(st + ab * kPanel + j * kOzGT * kRec + sl * kOzGT * 16 + k * 1024), 16,
+          lane * 16,
           __builtin_amdgcn_readfirstlane(soff), 0, 0);
     }
   };
@@ -182,23 +185,25 @@ __global__ __launch_bounds__(512, 1) void wide_oz_gram_kernel(const WideArgs a, 
     if (s + 2 < nsteps) issue(s + 2);
     if (!idle) {
       const char* st = smem + (s % kOzStages) * 2 * kPanel;
-      const char* pa = st + gq * kOzGT * kRec + (64 * qi + fi) * kRec;
-      const char* pb = st + kPanel + gq * kOzGT * kRec + (32 * qj + fi) * kRec;
+      // slices of this lane group's rowblock: [3][128 features][16 B]
+      const char* pa = st + gq * kOzGT * kRec + (64 * qi + fi) * 16;
+      const char* pb = st + kPanel + gq * kOzGT * kRec + (32 * qj + fi) * 16;
       oz_i4 Bq[2][5];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         u2 d[5];
 #pragma unroll
-        for (int b = 0; b < 5; ++b) d[b] = *(const u2*)(pb + u * 16 * kRec + 8 * b);
+        for (int b = 0; b < 5; ++b)
+          d[b] = *(const u2*)(pb + u * 16 * 16 + (b >> 1) * kOzGT * 16 + 8 * (b & 1));
         Bq[u][0] = oz_i4{(int)d[0].x, (int)d[0].y, 0, 0};
 #pragma unroll
         for (int b = 1; b < 5; ++b) Bq[u][b] = oz_i4{(int)d[b].x, (int)d[b].y, (int)d[b - 1].x, (int)d[b - 1].y};
       }
 #pragma unroll
       for (int si = 0; si < 4; ++si) {
-        const char* ra = pa + si * 16 * kRec;
-        const oz_i4 a0 = *(const oz_i4*)ra, a2 = *(const oz_i4*)(ra + 16);
-        const u2 a4v = *(const u2*)(ra + 32);
+        const char* ra = pa + si * 16 * 16;
+        const oz_i4 a0 = *(const oz_i4*)ra, a2 = *(const oz_i4*)(ra + kOzGT * 16);
+        const u2 a4v = *(const u2*)(ra + 2 * kOzGT * 16);
         const oz_i4 a4 = oz_i4{(int)a4v.x, (int)a4v.y, 0, 0};
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
