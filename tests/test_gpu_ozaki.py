@@ -118,15 +118,21 @@ def test_ozaki_bit_identical_runs(torch_cuda, M):
     assert torch.equal(f1.sig_inv, f2.sig_inv) and torch.equal(f1.theta, f2.theta)
 
 
-@pytest.mark.parametrize("case", ["fp64_mode", "long_chunks", "wide_p"])
+@pytest.mark.parametrize("case", ["fp64_mode", "long_chunks", "wide_p", "wide_long_groups",
+                                  "wide_fp64_mode"])
 def test_ozaki_fallbacks_keep_the_fp64_pass(torch_cuda, M, case):
-    """hessian="fp64" (no bf16 pass records the scales), chunks over 32767
-    rows (int32 level sums) and P > 112: the fp64-MFMA exact pass, same parity."""
+    """hessian="fp64" (no bf16 pass records the scales), chunks or wide Gram
+    row groups over 32767 rows (int32 level sums) and 112 < P <= 192: the
+    fp64-MFMA exact pass / Gram, same parity."""
     p, sizes, kw = 12, [40000, 36000], {"rows_per_chunk": 40000}
     if case == "fp64_mode":
         kw = {"hessian": "fp64", "rows_per_chunk": 3000}
     elif case == "wide_p":
         p, sizes, kw = 120, [6000, 5000], {"rows_per_chunk": 2000}
+    elif case == "wide_long_groups":
+        p, sizes, kw = 200, [34000, 3000], {"rows_per_chunk": 34000}
+    elif case == "wide_fp64_mode":
+        p, sizes, kw = 200, [6000, 5000], {"hessian": "fp64", "rows_per_chunk": 2000}
     X, y = O.simulate_counter(sum(sizes), p, seed=5 + p)
     off = np.concatenate([[0], np.cumsum(sizes)])
     fit = M.logistic_model_batched(X, y, off, **kw)
