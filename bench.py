@@ -396,14 +396,20 @@ def main():
                 "GBps": rows32 * row_bytes / (ms32 * 1e-3) / 1e9,
                 "alg_TFps": rows32 * p * (p + 1) / (ms32 * 1e-3) / 1e12,
                 "mfma_TFps": rows32 * gram_flops_row / (ms32 * 1e-3) / 1e12}
+        n_oz = tot("passes_oz")
+        gram_name = ("wide_oz_gram (int8 digit slices: scale + digits + 128x128 tiles)" if n_oz
+                     else "wide_gram_kernel<fp64>")
         if n64:
-            kern["wide_gram_kernel<fp64>"] = {
+            kern[gram_name] = {
                 "launches_per_step": n64 / args.steps, "avg_launch_ms": ms64 / n64,
                 "alg_TFps": rows64 * p * (p + 1) / (ms64 * 1e-3) / 1e12,
                 "mfma_TFps": rows64 * gram_flops_row / (ms64 * 1e-3) / 1e12}
+            if n_oz:
+                kern[gram_name]["note"] = ("DESIGN.md 4.4b; *_TFps count the fp64-equivalent "
+                                           "Gram work")
         kern["wide_assemble_kernel"] = {"ms_per_step": tot("ms_wide_assemble") / args.steps}
         kern["wide_newton_kernel"] = {"ms_per_step": tot("ms_solve") / args.steps}
-        if ms64 >= ms32:
+        if ms64 >= ms32 and not n_oz:
             achieved = rows64 * p * (p + 1) / (ms64 * 1e-3) / 1e12
             roof = {"kernel": "wide_gram_kernel<fp64> (X^T W X, 128x128 tiles)", "bound": "mfma",
                     "achieved": achieved, "peak": FP64_MFMA_PEAK_TF, "unit": "TFLOP/s",
