@@ -401,8 +401,9 @@ void dlsa_fit_options_default(dlsa_fit_options* opt) {
 const char* dlsa_last_error(void) { return g_last_error.c_str(); }
 
 const char* dlsa_build_info(void) {
-  return "libdlsa_hip gfx950 (CDNA4): cooperative fused IRLS pass (shared LDS-DMA ring, "
-         "bf16 16x16x32 / f64 16x16x4 MFMA), LDS Cholesky Newton update, host LARS";
+  return "libdlsa_hip gfx950 (CDNA4): fused IRLS passes over an LDS-DMA ring (bf16 16x16x32 "
+         "approximate Hessians; exact Hessians as int8 16x16x64 digit-slice sums or f64 "
+         "16x16x4 MFMA), wide 128x128 Gram tiles, LDS Cholesky Newton update, host LARS";
 }
 
 int64_t dlsa_logistic_workspace_bytes(const int64_t* offsets, int32_t K, int32_t p,
