@@ -110,9 +110,42 @@ struct Chol {
   // solve R^T x = b (forward)
   // (column-oriented: row k of R is contiguous; x[i] still subtracts its
   // terms in k order, so the rounding is that of the dot-product form)
+  // Four columns per sweep: the block's four entries are finalised in order,
+  // then the rest of x takes the four columns' updates in one pass (each
+  // element still subtracts them in k order, so the result is bitwise that of
+  // the one-column sweep, with a quarter of the dependent store-load chain).
   void solve_rt(const double* b, double* x) const {
     for (int i = 0; i < d; ++i) x[i] = b[i];
-    for (int k = 0; k < d; ++k) {
+    int k = 0;
+    for (; k + 4 <= d; k += 4) {
+      const double* r0 = &r[(size_t)k * m];
+      const double* r1 = r0 + m;
+      const double* r2 = r1 + m;
+      const double* r3 = r2 + m;
+      const double x0 = x[k] / r0[k];
+      x[k] = x0;
+      x[k + 1] += -x0 * r0[k + 1];
+      x[k + 2] += -x0 * r0[k + 2];
+      x[k + 3] += -x0 * r0[k + 3];
+      const double x1 = x[k + 1] / r1[k + 1];
+      x[k + 1] = x1;
+      x[k + 2] += -x1 * r1[k + 2];
+      x[k + 3] += -x1 * r1[k + 3];
+      const double x2 = x[k + 2] / r2[k + 2];
+      x[k + 2] = x2;
+      x[k + 3] += -x2 * r2[k + 3];
+      const double x3 = x[k + 3] / r3[k + 3];
+      x[k + 3] = x3;
+      for (int j = k + 4; j < d; ++j) {
+        double v = x[j];
+        v += -x0 * r0[j];
+        v += -x1 * r1[j];
+        v += -x2 * r2[j];
+        v += -x3 * r3[j];
+        x[j] = v;
+      }
+    }
+    for (; k < d; ++k) {
       const double xk = x[k] / at(k, k);
       x[k] = xk;
       axpy(d - k - 1, -xk, &r[(size_t)k * m + k + 1], x + k + 1);
@@ -121,9 +154,39 @@ struct Chol {
   // solve R x = b (backward), column-oriented on lt: x[i] is final once the
   // terms of x[i+1..d) are subtracted; each then updates x[0..i) with one
   // contiguous axpy (no per-row horizontal reduction on the recurrence)
+  // (blocked like solve_rt: four columns per sweep, same per-element order)
   void solve_r(const double* b, double* x) const {
     for (int i = 0; i < d; ++i) x[i] = b[i];
-    for (int i = d - 1; i >= 0; --i) {
+    int i = d - 1;
+    for (; i >= 3; i -= 4) {
+      const double* l0 = &lt[(size_t)i * m];
+      const double* l1 = l0 - m;
+      const double* l2 = l1 - m;
+      const double* l3 = l2 - m;
+      const double x0 = x[i] / l0[i];
+      x[i] = x0;
+      x[i - 1] += -x0 * l0[i - 1];
+      x[i - 2] += -x0 * l0[i - 2];
+      x[i - 3] += -x0 * l0[i - 3];
+      const double x1 = x[i - 1] / l1[i - 1];
+      x[i - 1] = x1;
+      x[i - 2] += -x1 * l1[i - 2];
+      x[i - 3] += -x1 * l1[i - 3];
+      const double x2 = x[i - 2] / l2[i - 2];
+      x[i - 2] = x2;
+      x[i - 3] += -x2 * l2[i - 3];
+      const double x3 = x[i - 3] / l3[i - 3];
+      x[i - 3] = x3;
+      for (int q = 0; q < i - 3; ++q) {
+        double v = x[q];
+        v += -x0 * l0[q];
+        v += -x1 * l1[q];
+        v += -x2 * l2[q];
+        v += -x3 * l3[q];
+        x[q] = v;
+      }
+    }
+    for (; i >= 0; --i) {
       const double* li = &lt[(size_t)i * m];
       const double xi = x[i] / li[i];
       x[i] = xi;
