@@ -671,7 +671,7 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
   woz.E = (int32_t*)at(L.off_ozE);
   woz.maxblk = (max_grows + 31) / 32;
   const int PPw = kWideTile * NB;
-  const size_t digit_bytes = (size_t)std::max(fg.n_chunks, 1) * woz.maxblk * 4 * PPw * 48;
+  const size_t digit_bytes = (size_t)std::max(fg.n_chunks, 1) * woz.maxblk * 4 * PPw * 40;
   const bool use_wide_oz = !(getenv("DLSA_OZ") && atoi(getenv("DLSA_OZ")) == 0) &&
                            family == FAMILY_LOGISTIC && opt.hessian_mode == DLSA_HESSIAN_MIXED &&
                            max_grows <= kWideOzMaxRows && digit_bytes <= (size_t(32) << 30);

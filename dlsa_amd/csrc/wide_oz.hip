@@ -12,10 +12,11 @@
 //   wide_oz_digits_kernel  F = round(z 2^(38 - E_f)) by one FMA against
 //                        1.5 2^52 + 0x8080808080; its five bytes XOR 0x80 are
 //                        balanced digits d_0 .. d_4 (byte r of plane d = digit
-//                        d of row r), stored per 8 rows as three slices of
-//                        [feature][16 B] (planes 0-1, 2-3, 4): a wave's store
-//                        of a slice is 1 KB contiguous, and the consumers'
-//                        fragment reads are 16-byte strided (no bank conflicts)
+//                        d of row r), stored per 8 rows as three slices
+//                        [feature][16 B] (planes 0-1), [feature][16 B] (2-3),
+//                        [feature][8 B] (4): 40 bytes per (8 rows, feature), a
+//                        wave's store of a slice is contiguous, and the
+//                        consumers' fragment reads are 16- / 8-byte strided
 //   wide_oz_gram_kernel  per (row group, 128 x 128 tile): 8 waves, each a
 //                        64 x 32 block (4 x 2 sub-tiles of 16 x 16), NL = 5
 //                        int32 level accumulators per sub-tile; per 32-row step
@@ -31,10 +32,11 @@ namespace dlsa {
 
 namespace {
 
-constexpr int kRec = ozk::kFeatBytes;  // 48-byte digit record (5 planes + pad)
+constexpr int kRec = 40;               // digit bytes per (8 rows, feature): 5 planes
 constexpr int kOzGT = 128;             // output tile edge
 constexpr int kOzStages = 3;           // LDS ring: 2 steps in flight + 1 computed
-constexpr int kPanel = 4 * kOzGT * kRec;  // one panel of a step: 4 x 128 records
+constexpr int kPanel = 4 * kOzGT * kRec;  // one panel of a step: 4 rowblocks x 128 features (20 KB)
+constexpr int kPieces = kPanel / 1024;    // 1-KB DMA pieces of a panel (20)
 
 }  // namespace
 
@@ -101,7 +103,8 @@ __global__ __launch_bounds__(256) void wide_oz_digits_kernel(const WideArgs a, c
       const uint32_t p23 = __builtin_amdgcn_perm(src[r0 + 3], src[r0 + 2], sel);
       return __builtin_amdgcn_perm(p23, p01, 0x05040100u) ^ 0x80808080u;
     };
-    uint4 q0, q1, q2;
+    uint4 q0, q1;
+    uint2 q2;
     q0.x = pack(hi, 0, 0);
     q0.y = pack(hi, 0, 4);
     q0.z = pack(lo, 3, 0);
@@ -112,12 +115,10 @@ __global__ __launch_bounds__(256) void wide_oz_digits_kernel(const WideArgs a, c
     q1.w = pack(lo, 1, 4);
     q2.x = pack(lo, 0, 0);
     q2.y = pack(lo, 0, 4);
-    q2.z = 0u;
-    q2.w = 0u;
     uint4* dst = (uint4*)(rec + (int64_t)f * 16);
     dst[0] = q0;
     dst[PP] = q1;
-    dst[2 * PP] = q2;
+    *(uint2*)(rec + 32 * PP + (int64_t)f * 8) = q2;
   }
 }
 
@@ -150,18 +151,22 @@ __global__ __launch_bounds__(512, 1) void wide_oz_gram_kernel(const WideArgs a, 
   const __amdgpu_buffer_rsrc_t dr =
       wv_rsrc(gbase, (uintptr_t)o.maxblk * 4 * PP * kRec);
   const int stepb = 4 * PP * kRec;
-  // this wave's DMA pieces of a step: 48 x 1 KB (A: 24, B: 24), 6 per wave
+  // this wave's DMA pieces of a step: 40 x 1 KB (A: 20, B: 20), 5 per wave;
+  // a rowblock's panel is 5 KB: slices 0 and 1 (2 KB each), slice 2 (1 KB)
   auto issue = [&](int s) {
     char* st = smem + (s % kOzStages) * 2 * kPanel;
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      const int pc = wid * 6 + i;        // 0 .. 47
-      const int ab = pc / 24, q = pc % 24;  // panel, piece within it
-      const int j = q / 6, sl = (q % 6) >> 1, k = q & 1;  // rowblock, slice, 1 KB half
-      const int soff = s * stepb + j * PP * kRec + sl * PP * 16 + (ab ? J : I) * kOzGT * 16 + k * 1024;
+    for (int i = 0; i < 5; ++i) {
+      const int pc = wid * 5 + i;              // 0 .. 39
+      const int ab = pc / kPieces, q = pc % kPieces;  // panel, piece within it
+      const int j = q / 5, e = q % 5;         // rowblock, piece within its 5 KB
+      const int sl = e >> 1;                   // slice (0, 1: two pieces; 2: one)
+      const int k = e & 1;
+      const int src = sl < 2 ? sl * PP * 16 + (ab ? J : I) * kOzGT * 16 + k * 1024
+                             : 32 * PP + (ab ? J : I) * kOzGT * 8;
+      const int soff = s * stepb + j * PP * kRec + src;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          dr, (wlds_void_t*)(st + ab * kPanel + j * kOzGT * kRec + sl * kOzGT * 16 + k * 1024), 16,
-          lane * 16,
+          dr, (wlds_void_t*)(st + ab * kPanel + j * kOzGT * kRec + e * 1024), 16, lane * 16,
           __builtin_amdgcn_readfirstlane(soff), 0, 0);
     }
   };
@@ -177,7 +182,7 @@ __global__ __launch_bounds__(512, 1) void wide_oz_gram_kernel(const WideArgs a, 
   issue(0);
   if (nsteps > 1) issue(1);
   if (nsteps > 1)
-    wv_wait_vmcnt<6>();
+    wv_wait_vmcnt<5>();
   else
     wv_wait_vmcnt<0>();
   ozk::barrier();
@@ -188,13 +193,17 @@ __global__ __launch_bounds__(512, 1) void wide_oz_gram_kernel(const WideArgs a, 
       // slices of this lane group's rowblock: [3][128 features][16 B]
       const char* pa = st + gq * kOzGT * kRec + (64 * qi + fi) * 16;
       const char* pb = st + kPanel + gq * kOzGT * kRec + (32 * qj + fi) * 16;
+      // slice 2 (plane 4): 8 bytes per feature after the two 2-KB slices
+      const char* pa2 = st + gq * kOzGT * kRec + 4096 + (64 * qi + fi) * 8;
+      const char* pb2 = st + kPanel + gq * kOzGT * kRec + 4096 + (32 * qj + fi) * 8;
       oz_i4 Bq[2][5];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         u2 d[5];
 #pragma unroll
-        for (int b = 0; b < 5; ++b)
+        for (int b = 0; b < 4; ++b)
           d[b] = *(const u2*)(pb + u * 16 * 16 + (b >> 1) * kOzGT * 16 + 8 * (b & 1));
+        d[4] = *(const u2*)(pb2 + u * 16 * 8);
         Bq[u][0] = oz_i4{(int)d[0].x, (int)d[0].y, 0, 0};
 #pragma unroll
         for (int b = 1; b < 5; ++b) Bq[u][b] = oz_i4{(int)d[b].x, (int)d[b].y, (int)d[b - 1].x, (int)d[b - 1].y};
@@ -203,7 +212,7 @@ __global__ __launch_bounds__(512, 1) void wide_oz_gram_kernel(const WideArgs a, 
       for (int si = 0; si < 4; ++si) {
         const char* ra = pa + si * 16 * 16;
         const oz_i4 a0 = *(const oz_i4*)ra, a2 = *(const oz_i4*)(ra + kOzGT * 16);
-        const u2 a4v = *(const u2*)(ra + 2 * kOzGT * 16);
+        const u2 a4v = *(const u2*)(pa2 + si * 16 * 8);
         const oz_i4 a4 = oz_i4{(int)a4v.x, (int)a4v.y, 0, 0};
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
@@ -222,7 +231,7 @@ __global__ __launch_bounds__(512, 1) void wide_oz_gram_kernel(const WideArgs a, 
     }
     // step s+1 landed (s+2 may stay in flight); everyone done with stage s
     if (s + 2 < nsteps)
-      wv_wait_vmcnt<6>();
+      wv_wait_vmcnt<5>();
     else
       wv_wait_vmcnt<0>();
     ozk::barrier();  // (not __syncthreads: its fence would drain step s+2's DMA)
