@@ -51,6 +51,8 @@ sys.path.insert(0, ROOT)
 METRIC = "DLSA logistic fit rows/sec (node), n=1e8 p=100, 1/2/4/8 GPUs; HBM GB/s"
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
 FP64_MFMA_PEAK_TF = 78.6   # MI355X fp64 matrix (spec; = fp64 vector on CDNA4)
+I8_MFMA_PEAK_TOPS = 5000.0  # int8 dense: 2x the ~2.5 PF bf16 dense rate (MI355X_MICROARCH.md
+#                             "Matrix cores": i8 16x16x64 = the bf16 cycles at 2x the K)
 
 CONFIGS = {
     2: dict(n=100_000_000, p=100, K=1024, family="logistic",
@@ -205,6 +207,9 @@ def main():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group transport for N > 1 (nccl = RCCL over xGMI; gloo: "
                          "host transport, lets several ranks share one GPU in tests)")
+    ap.add_argument("--force-pg", action="store_true",
+                    help="create the process group (--backend) even at --gpus 1, so the "
+                         "combine runs its all-reduce (RCCL at one rank)")
     ap.add_argument("--n", type=int, default=0, help="rows (per GPU, or total when strong)")
     ap.add_argument("--p", type=int, default=0)
     ap.add_argument("--partitions", type=int, default=0)
@@ -245,7 +250,16 @@ def main():
                          "--backend gloo lets ranks share a GPU")
     torch.cuda.set_device(local % ndev)
     dev = torch.device("cuda", local % ndev)
-    if world > 1:
+    use_pg = world > 1 or args.force_pg
+    if use_pg:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if "MASTER_PORT" not in os.environ:
+            import socket
+            with socket.socket() as s_:
+                s_.bind(("127.0.0.1", 0))
+                os.environ["MASTER_PORT"] = str(s_.getsockname()[1])
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", str(world))
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -316,7 +330,8 @@ def main():
                 ws = torch.empty((fit.stats["workspace_bytes"],), dtype=torch.uint8, device=dev)
         t_b = time.perf_counter()  # the fit returns after its stream synchronisation
         buf = reduce_partitions_device(fit, n_rows=True)
-        combine(buf)  # the one collective: RCCL all-reduce over xGMI (no-op at N = 1)
+        combine(buf)  # the one collective: RCCL all-reduce over xGMI (none at N = 1
+        #                without --force-pg)
         b = buf.cpu().numpy()
         t_c = time.perf_counter()
         S, v, st, Ksum = split_reduced(b[:-1], fit.P)
@@ -334,17 +349,17 @@ def main():
     for _ in range(args.warmup):
         step(False)
     torch.cuda.synchronize()
-    if world > 1:
+    if use_pg:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         fit, est, support, K_red, n_red = step(True)
         stats_acc.append(fit.stats)
     torch.cuda.synchronize()
-    if world > 1:
+    if use_pg:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if use_pg:
         t = torch.tensor([elapsed], dtype=torch.float64,
                          device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -405,8 +420,18 @@ def main():
                 "alg_TFps": rows64 * p * (p + 1) / (ms64 * 1e-3) / 1e12,
                 "mfma_TFps": rows64 * gram_flops_row / (ms64 * 1e-3) / 1e12}
             if n_oz:
-                kern[gram_name]["note"] = ("DESIGN.md 4.4b; *_TFps count the fp64-equivalent "
-                                           "Gram work")
+                # 72 v_mfma_i32_16x16x64_i8 per wave (8 waves) per 32 rows per 128x128
+                # tile: 9 per 16x16 sub-tile, diagonal tiles' upper quadrants idle
+                tiles = NB * (NB + 1) // 2
+                i8_ops_row = tiles * 8 * 72 * 16 * 16 * 64 * 2 / 32
+                tops = rows64 * i8_ops_row / (ms64 * 1e-3) / 1e12
+                del kern[gram_name]["mfma_TFps"]
+                kern[gram_name].update({
+                    "int8_mfma_TOPS_issued_upper_bound": tops,
+                    "int8_mfma_frac_upper_bound": tops / I8_MFMA_PEAK_TOPS,
+                    "note": "DESIGN.md 4.4b: scale + digits + 128x128 int8 tiles; alg_TFps "
+                            "counts the fp64-equivalent Gram work; the int8 rate counts every "
+                            "tile's MFMAs as issued (the idle diagonal quadrants included)"})
         kern["wide_assemble_kernel"] = {"ms_per_step": tot("ms_wide_assemble") / args.steps}
         kern["wide_newton_kernel"] = {"ms_per_step": tot("ms_solve") / args.steps}
         if ms64 >= ms32 and not n_oz:
@@ -439,17 +464,24 @@ def main():
                 "GBps": rows32 * row_bytes / (ms32 * 1e-3) / 1e9,
                 "mfma_TFps": rows32 * mfma_flops_per_row / (ms32 * 1e-3) / 1e12}
         if n64:
+            gbps = rows64 * row_bytes / (ms64 * 1e-3) / 1e9
             kern[exact] = {
                 "launches_per_step": n64 / args.steps, "ms_per_step": ms64 / args.steps,
                 "avg_launch_ms": ms64 / n64, "rows_per_launch": rows64 / n64,
-                "GBps": rows64 * row_bytes / (ms64 * 1e-3) / 1e9,
-                "alg_TFps": rows64 * alg_flops_row / (ms64 * 1e-3) / 1e12,
-                "mfma_TFps": rows64 * mfma_flops_per_row / (ms64 * 1e-3) / 1e12,
-                "mfma_frac": rows64 * mfma_flops_per_row / (ms64 * 1e-3) / 1e12
-                / FP64_MFMA_PEAK_TF}
-            if n_oz:  # the Hessian runs on the int8 matrix cores: bytes bound the pass
-                kern[exact]["note"] = ("X^T W X as int8 digit-slice products (DESIGN.md 4.1c); "
-                                       "mfma_* count the fp64-equivalent tile work")
+                "GBps": gbps, "hbm_frac": gbps / HBM_PEAK_GBS,
+                "alg_TFps": rows64 * alg_flops_row / (ms64 * 1e-3) / 1e12}
+            if n_oz:
+                # the Hessian runs on the int8 matrix cores: 9 v_mfma_i32_16x16x64_i8 per
+                # lower-triangle 16x16 tile per 32 rows, 32768 ops each
+                i8_ops_row = NT * (NT + 1) // 2 * 9 * 16 * 16 * 64 * 2 / 32
+                tops = rows64 * i8_ops_row / (ms64 * 1e-3) / 1e12
+                kern[exact].update({"int8_mfma_TOPS": tops,
+                                    "int8_mfma_frac": tops / I8_MFMA_PEAK_TOPS,
+                                    "note": "X^T W X as int8 digit-slice products (5 levels of "
+                                            "a 38-bit grid, DESIGN.md 4.1c); bound: HBM"})
+            else:
+                tf = rows64 * mfma_flops_per_row / (ms64 * 1e-3) / 1e12
+                kern[exact].update({"mfma_TFps": tf, "mfma_frac": tf / FP64_MFMA_PEAK_TF})
         kern["newton_solve"] = {"ms_per_step": tot("ms_solve") / args.steps}
         if ms32 >= ms64:
             roof = hbm_roof(f"irls_coop_kernel<NT={NT},bf16 Hessian> (approximate-Hessian "
@@ -458,8 +490,12 @@ def main():
         elif family == "ols":
             # config 4 is HBM-bound (65 GB vs 0.54 TF per GPU)
             roof = hbm_roof(exact + " (OLS: X^T X, X^T y in one pass)", ms64, n64, rows64)
-            roof["mfma_issued_frac"] = kern[exact]["mfma_frac"]
+            roof["mfma_issued_frac"] = kern[exact].get("mfma_frac")
             pmc_key = "irls_wave<ols>"
+        elif n_oz:  # the int8 exact pass streams X once: HBM-bound
+            roof = hbm_roof(exact, ms64, n64, rows64)
+            roof["int8_mfma_frac"] = kern[exact]["int8_mfma_frac"]
+            pmc_key = "irls_oz"
         else:
             achieved = rows64 * mfma_flops_per_row / (ms64 * 1e-3) / 1e12
             roof = {"kernel": exact, "bound": "mfma", "achieved": achieved,
@@ -488,6 +524,14 @@ def main():
             pass
 
     last = stats_acc[-1]
+    # the arithmetic of the published Sig_inv (dtype "f64" is the data and the
+    # gradient; the exact Hessian may be int8-Ozaki emulated)
+    if last.get("passes_oz", 0):
+        sig_inv_arith = "int8-ozaki-5L (38-bit digit grid, 5 levels; ~1e-12 relative)"
+    elif codes_layout:
+        sig_inv_arith = "fp64 + int64 fixed-point LDS histograms"
+    else:
+        sig_inv_arith = "fp64-mfma"
     out = {
         "metric": METRIC, "value": value, "unit": "rows/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
@@ -507,11 +551,12 @@ def main():
                    **({"layout": args.layout} if data == "dummy" else {}),
                    "family": family,
                    "hessian": args.hessian if family == "logistic" and not codes_layout else "fp64",
+                   "sig_inv": sig_inv_arith,
                    "tol": args.tol,
                    "parallelism": f"dp{world} (partitions sharded; 1 "
                                   f"{'RCCL' if args.backend == 'nccl' else 'gloo'} all-reduce of "
                                   "P^2+2P+2 fp64)",
-                   "backend": args.backend if world > 1 else None},
+                   "backend": args.backend if use_pg else None},
         "roofline": roof,
         "kernels": kern,
         "stages_ms_per_step": dict({k: v / args.steps for k, v in stage_ms.items()},
@@ -543,7 +588,7 @@ def main():
         out["vs_cpu_baseline"] = value / out["cpu_baseline"]["value"]
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_pg:
         dist.destroy_process_group()
 
 

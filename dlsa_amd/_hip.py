@@ -61,6 +61,7 @@ class FitStats(ctypes.Structure):
         ("passes_f32x", ctypes.c_int32),
         ("polish_partitions", ctypes.c_int32),
         ("passes_oz", ctypes.c_int32),
+        ("oz_fallbacks", ctypes.c_int32),
     ]
 
     def as_dict(self):

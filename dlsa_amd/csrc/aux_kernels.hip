@@ -102,6 +102,24 @@ hipError_t launch_fit_finalize(int K, int P, const double* theta, const double* 
   return hipGetLastError();
 }
 
+// theta_rec[k] = theta[k] for the partitions whose phase is ph: the point at
+// which the next bf16 pass records their Ozaki digit scales
+__global__ void theta_snapshot_kernel(int K, int P, const int32_t* phase, int ph,
+                                      const double* theta, double* theta_rec) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)K * P) return;
+  if (phase[i / P] == ph) theta_rec[i] = theta[i];
+}
+
+hipError_t launch_theta_snapshot(int K, int P, const int32_t* phase, int ph, const double* theta,
+                                 double* theta_rec, hipStream_t s) {
+  const int64_t n = (int64_t)K * P;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(theta_snapshot_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, K,
+                     P, phase, ph, theta, theta_rec);
+  return hipGetLastError();
+}
+
 // out = [sum_k Sig_inv_k | sum_k Sig_inv_k theta_k | sum_k theta_k | K]
 // One thread per output element, partitions summed in index order.  The
 // loads run 16 partitions ahead of the (sequential, order-preserving) adds:

@@ -142,22 +142,6 @@ static int32_t* pinned_staging(size_t n_i32) {
   return buf;
 }
 
-// Device buffer of the wide path's int8 digit records (wide_oz.hip), grown on
-// demand and kept for the process (several GB at config 5: no allocation and
-// mapping per fit).
-static int8_t* digit_buffer(size_t bytes) {
-  static int8_t* buf = nullptr;
-  static size_t cap = 0;
-  if (cap < bytes) {
-    if (buf) (void)hipFree(buf);
-    buf = nullptr;
-    cap = 0;
-    if (hipMalloc((void**)&buf, bytes) != hipSuccess) return nullptr;
-    cap = bytes;
-  }
-  return buf;
-}
-
 static double warm_level_tol(bool fused) {
   if (const char* e = getenv("DLSA_LEVEL_TOL")) return atof(e);
   return fused ? 0.2 : 0.1;
@@ -209,7 +193,7 @@ struct Layout {
   int64_t off_slabH, off_slabg, off_slabll;
   int64_t off_phase, off_bt, off_llprev, off_thprev, off_dprev, off_counters;
   int64_t off_dmprev, off_stall;
-  int64_t off_colmax;
+  int64_t off_colmax, off_zcolmax, off_threc;  // Ozaki digit scales (PassArgs)
   int64_t total;
 };
 
@@ -238,6 +222,8 @@ static Layout make_layout(const Plan& pl, int K) {
   L.off_dmprev = take(8LL * K);
   L.off_stall = take(4LL * K);
   L.off_colmax = take(4LL * std::max(pl.n_chunks, 1) * pl.PP);
+  L.off_zcolmax = take(4LL * std::max(pl.n_chunks, 1) * pl.PP);
+  L.off_threc = take(8LL * K * pl.P);
   L.total = o;
   return L;
 }
@@ -282,9 +268,17 @@ struct WideLayout {
   int64_t off_phase, off_bt, off_llprev, off_thprev, off_dprev, off_counters;
   int64_t off_dmprev, off_stall;
   int64_t off_zmax, off_ozE;  // int8 exact Gram: row-chunk max |z|, digit exponents
+  // int8 exact Gram digit records (wide_oz.hip): the last region, so that
+  // base_total bytes hold everything else; digit_bytes = 0 when the final
+  // plan's row groups are too long (> kWideOzMaxRows) or the records would
+  // exceed kWideOzMaxDigitBytes (the fp64 Gram runs then)
+  int64_t off_digits, digit_bytes, base_total;
   int64_t total;
   int64_t cap_rows, cap_gram;  // row-chunk / Gram-row-group capacity of the tables and slabs
 };
+
+// Largest digit-record region a wide fit asks for (above it: fp64 Gram).
+constexpr int64_t kWideOzMaxDigitBytes = int64_t(32) << 30;
 
 // Sized for the largest chunk counts over ALL level plans: a warm-start
 // level's row groups are sized from its own (smaller) row count, so with
@@ -332,7 +326,14 @@ static WideLayout make_wide_layout(const std::vector<WidePlans>& plans, int K, i
   L.off_dmprev = take(8LL * K);
   L.off_stall = take(4LL * K);
   L.off_zmax = take(4 * nr * PP);
-  L.off_ozE = take(4LL * K * PP);
+  L.off_ozE = take(4 * ng * PP);
+  L.base_total = o;
+  const Plan& fg = plans.back().gram;
+  int max_grows = 0;
+  for (int c = 0; c < fg.n_chunks; ++c) max_grows = std::max(max_grows, fg.chunk_rows[c]);
+  const int64_t db = wide_oz_digit_bytes(fg.n_chunks, max_grows, (int)PP);
+  L.digit_bytes = (max_grows <= kWideOzMaxRows && db <= kWideOzMaxDigitBytes) ? db : 0;
+  L.off_digits = take(L.digit_bytes);
   L.total = o;
   L.cap_rows = nr;
   L.cap_gram = ng;
@@ -543,14 +544,43 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
   const WideLayout L = make_wide_layout(plans, K, n_total, P);
   g_stats.n_chunks = plans.back().gram.n_chunks;
 
+  // The exact Gram pass runs on the int8 matrix cores (wide_oz.hip) in mixed
+  // mode when the final plan's row groups are <= kWideOzMaxRows rows and its
+  // digit records fit the workspace: the caller's (dlsa_logistic_workspace_bytes
+  // counts them) or the one allocated here.  Without room for them -- a
+  // caller workspace of at least base_total but less than total bytes, a
+  // failed allocation, or DLSA_WIDE_OZ_MAX_BYTES below the records' size --
+  // the fp64 Gram runs (stats.oz_fallbacks).  DLSA_OZ=0: always the fp64 Gram.
+  bool use_wide_oz = !(getenv("DLSA_OZ") && atoi(getenv("DLSA_OZ")) == 0) &&
+                     family == FAMILY_LOGISTIC && opt.hessian_mode == DLSA_HESSIAN_MIXED &&
+                     L.digit_bytes > 0;
+  if (use_wide_oz)
+    if (const char* e = getenv("DLSA_WIDE_OZ_MAX_BYTES"))
+      if (L.digit_bytes > atoll(e)) {
+        use_wide_oz = false;
+        g_stats.oz_fallbacks++;
+      }
   char* ws = (char*)opt.workspace;
   bool owned = false;
   if (!ws) {
-    DLSA_HIP_TRY(hipMallocAsync((void**)&ws, L.total, stream));
+    hipError_t e = hipErrorOutOfMemory;
+    if (use_wide_oz) {
+      e = hipMallocAsync((void**)&ws, L.total, stream);
+      if (e != hipSuccess) {
+        (void)hipGetLastError();  // out of memory: the fp64 Gram needs no records
+        ws = nullptr;
+        use_wide_oz = false;
+        g_stats.oz_fallbacks++;
+      }
+    }
+    if (!ws) DLSA_HIP_TRY(hipMallocAsync((void**)&ws, L.base_total, stream));
     owned = true;
-  } else if (opt.workspace_bytes < L.total) {
+  } else if (opt.workspace_bytes < L.base_total) {
     set_error("workspace too small: need " + std::to_string(L.total) + " bytes");
     return DLSA_E_WORKSPACE;
+  } else if (use_wide_oz && opt.workspace_bytes < L.total) {
+    use_wide_oz = false;
+    g_stats.oz_fallbacks++;
   }
   struct Free {
     char* p;
@@ -656,11 +686,9 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
   }
   int32_t* h_phase = h_cnt + 4;  // [K] phases (pinned: no staging copy per iteration)
 
-  // The exact Gram pass: on the int8 matrix cores (wide_oz.hip) in mixed mode
-  // when every Gram row group of the final plan is <= 32767 rows and the digit
-  // records fit their budget (DLSA_OZ=0: always the fp64 Gram).  The row pass
-  // then also records each chunk's max |sqrt(w) x|, from which the scale kernel
-  // takes the digit exponents.
+  // The row pass of an int8 exact Gram also records each row chunk's max
+  // |sqrt(w) x|, from which the scale kernel takes the digit exponents of
+  // every Gram row group.
   const Plan& fg = plans.back().gram;
   int max_grows = 0;
   for (int c = 0; c < fg.n_chunks; ++c) max_grows = std::max(max_grows, fg.chunk_rows[c]);
@@ -670,18 +698,7 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
   woz.zmax = (const uint32_t*)at(L.off_zmax);
   woz.E = (int32_t*)at(L.off_ozE);
   woz.maxblk = (max_grows + 31) / 32;
-  const int PPw = kWideTile * NB;
-  const size_t digit_bytes = (size_t)std::max(fg.n_chunks, 1) * woz.maxblk * 4 * PPw * 40;
-  const bool use_wide_oz = !(getenv("DLSA_OZ") && atoi(getenv("DLSA_OZ")) == 0) &&
-                           family == FAMILY_LOGISTIC && opt.hessian_mode == DLSA_HESSIAN_MIXED &&
-                           max_grows <= kWideOzMaxRows && digit_bytes <= (size_t(32) << 30);
-  if (use_wide_oz) {
-    woz.D = digit_buffer(digit_bytes);
-    if (!woz.D) {
-      set_error("digit buffer allocation failed");
-      return DLSA_E_HIP;
-    }
-  }
+  woz.D = use_wide_oz ? (int8_t*)at(L.off_digits) : nullptr;
   auto exact_gram = [&](const WidePlans& q, bool final_level) -> hipError_t {
     const bool oz = use_wide_oz && final_level;
     wa.slab_zmax = oz ? (uint32_t*)at(L.off_zmax) : nullptr;
@@ -698,7 +715,7 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
     return timed(
         &g_stats.ms_wide_gram,
         [&] {
-          hipError_t e2 = launch_wide_oz_scale(wa, woz, K, stream);
+          hipError_t e2 = launch_wide_oz_scale(wa, woz, stream);
           if (e2 == hipSuccess) e2 = launch_wide_oz_digits(wa, woz, standardize, stream);
           if (e2 == hipSuccess) e2 = launch_wide_oz_gram(wa, woz, stream);
           return e2;
@@ -996,31 +1013,40 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
   const bool trace = getenv("DLSA_TRACE") != nullptr;
   int32_t* h_phase = h_cnt + 4;  // [K] phases (pinned: no staging copy per iteration)
   // exact passes on the int8 matrix cores (irls_oz_impl.hpp) unless DLSA_OZ=0:
-  // the fit's first full-data bf16 pass records every chunk's per-feature max
-  // |x| (the digit scales), after which the exact passes of the final plan
-  // take the Ozaki kernel
+  // every full-data bf16 pass records, per chunk and feature, max |x| and max
+  // |sqrt(w) x| at the theta it saw (snapshotted into theta_rec first), and
+  // the exact passes of the final plan take their digit scales from the
+  // partition's last record
   const bool use_oz = !(getenv("DLSA_OZ") && atoi(getenv("DLSA_OZ")) == 0) &&
                       approx_prec == PREC_BF16 && oz_applies(pl.NT, p) &&
                       pl.max_chunk_rows <= kOzMaxRows;
   uint32_t* d_colmax = (uint32_t*)at(L.off_colmax);
+  uint32_t* d_zcolmax = (uint32_t*)at(L.off_zcolmax);
+  double* d_threc = (double*)at(L.off_threc);
   bool colmax_ready = false;
   // one pass over the chunks of plan q whose partition is in phase ph:
   // exact (fp64 Hessian) passes by the per-wave kernel up to P = 128 and the
   // cooperative one above; approximate passes (PHASE_F32 at the fit's
   // approximate precision, PHASE_F32X at fp32) by the cooperative kernel
-  auto fused_pass = [&](int ph, const Plan& q, const std::vector<int64_t>& part_rows,
+  // (full: q is the all-rows plan, whose chunks the digit scales describe)
+  auto fused_pass = [&](int ph, const Plan& q, bool full, const std::vector<int64_t>& part_rows,
                         const int32_t* hph) -> hipError_t {
     const bool f64 = ph == PHASE_F64;
     const int prec = f64 ? PREC_F64 : (ph == PHASE_F32X ? PREC_F32 : approx_prec);
     pa.want_phase = ph;
     const bool wave = f64 && q.NT <= kWaveMaxNT;
-    const bool full = &q == &plans.back();
     const bool oz = wave && use_oz && colmax_ready && full;
-    // the first full-data bf16 pass records the digit scales
-    const bool record = use_oz && !colmax_ready && full && ph == PHASE_F32;
+    // every full-data bf16 pass records the digit scales
+    const bool record = use_oz && full && ph == PHASE_F32;
+    if (record) {
+      hipError_t e = launch_theta_snapshot(K, P, d_phase, PHASE_F32, theta, d_threc, stream);
+      if (e != hipSuccess) return e;
+    }
     hipError_t e = timed(f64 ? &g_stats.ms_pass_fp64 : &g_stats.ms_pass_fp32, [&] {
       PassArgs pc = pa;
       pc.colmax = (oz || record) ? d_colmax : nullptr;
+      pc.zcolmax = (oz || record) ? d_zcolmax : nullptr;
+      pc.theta_rec = d_threc;
       if (oz) return launch_irls_oz(pc, q.NT, standardize, family, q.n_chunks, stream);
       if (wave) return launch_irls_wave(pc, q.NT, standardize, family, q.n_chunks, stream);
       return launch_irls_coop(pc, q.NT, prec, standardize, family, q.n_chunks, stream);
@@ -1067,7 +1093,7 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
       // approximate (bf16 or fp32), escalated fp32, then exact passes
       for (int ph : {PHASE_F32, PHASE_F32X, PHASE_F64}) {
         if (n_running[ph] == 0) continue;
-        DLSA_HIP_TRY(fused_pass(ph, q, part_rows, h_phase));
+        DLSA_HIP_TRY(fused_pass(ph, q, final_level, part_rows, h_phase));
       }
       DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
       DLSA_HIP_TRY(timed(&g_stats.ms_solve, [&] { return launch_newton_solve(sa, K, stream); }));
@@ -1083,13 +1109,13 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
   // at the theta they return; its X^T W X is published as Sig_inv, no step
   // (models.py:114,130 evaluate the weights at the coef sklearn stopped at)
   if (family == FAMILY_LOGISTIC && running_total(n_running) > 0 && pl.n_chunks > 0) {
-    if (plans.size() > 1) DLSA_HIP_TRY(upload(pl));  // (already the last level's plan)
+    // (the final level's plan, pl, is on the device: it was the last uploaded)
     DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
     DLSA_HIP_TRY(launch_polish_mark(K, d_phase, status, d_cnt, stream));
     DLSA_HIP_TRY(hipMemcpyAsync(h_phase, d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
     DLSA_HIP_TRY(hipStreamSynchronize(stream));
     g_stats.polish_partitions = running_total(n_running);
-    DLSA_HIP_TRY(fused_pass(PHASE_F64, pl, plan_part_rows(pl, K), h_phase));
+    DLSA_HIP_TRY(fused_pass(PHASE_F64, plans.back(), true, plan_part_rows(pl, K), h_phase));
     sa.eval_only = 1;
     sa.subsample = 0;
     DLSA_HIP_TRY(timed(&g_stats.ms_solve, [&] { return launch_newton_solve(sa, K, stream); }));

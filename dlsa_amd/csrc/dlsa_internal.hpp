@@ -31,10 +31,12 @@ enum : int32_t { FAMILY_LOGISTIC = 0, FAMILY_GAUSSIAN = 1 };
 
 // Cache policy of the LDS-DMA loads that stream X (the aux / cpol operand of
 // buffer_load ... lds): X is read once per pass and is far larger than every
-// cache, so streaming it non-temporally (2 = nt) is the default candidate;
-// profiling builds override it (tools/build_variants.sh).
+// cache, so it streams non-temporally (2 = nt): config 2 76.3-76.9 vs
+// 77.6-77.9 ms per fit against the default policy in one A/B run
+// (profiles/r04a_nt_ab.txt); profiling builds override it
+// (tools/build_variants.sh).
 #ifndef DLSA_X_DMA_AUX
-#define DLSA_X_DMA_AUX 0
+#define DLSA_X_DMA_AUX 2
 #endif
 // Cooperative pass: 4 (8) waves per workgroup, 32-row blocks.
 constexpr int kCoopRows = 32;
@@ -63,10 +65,16 @@ struct PassArgs {
   int32_t want_phase;
   int32_t nslot;              // cooperative pass: LDS ring depth (32-row slots)
   int32_t slot_bytes;
-  // [n_chunks, 16*NT] per chunk and feature, max |x| (its fp64 high dword, after
-  // standardisation): written by a bf16 pass when set, read by the Ozaki
-  // exact pass (irls_oz_impl.hpp) as its digit scales
+  // Digit scales of the Ozaki exact pass (irls_oz_impl.hpp), written by the
+  // bf16 passes of the final level when set:
+  //   colmax  [n_chunks, 16*NT] per chunk and feature max |x| (the fp64 high
+  //           dword, after standardisation)
+  //   zcolmax [n_chunks, 16*NT] max |z|, z = sqrt(w) x at the pass's theta
+  //           (fp32 bits)
+  //   theta_rec [K, P] the theta of the partition's last recording pass
   uint32_t* colmax;
+  uint32_t* zcolmax;
+  const double* theta_rec;
 };
 
 // Arguments of the per-partition Newton update.
@@ -196,15 +204,25 @@ struct WideArgs {
 struct WideOzArgs {
   const int32_t* rcb;      // [K+1] row-pass chunks of each partition
   const uint32_t* zmax;    // [n_rchunks, PP] the row pass's max |sqrt(w) x| high dwords
-  int32_t* E;              // [K, PP] digit exponents
-  int8_t* D;               // digit records [n_gchunks][maxblk][4][PP][48]
+  int32_t* E;              // [n_gchunks, PP] digit exponents of each Gram row group
+  // digit records, part of the fit's workspace (WideLayout::off_digits):
+  // [n_gchunks][maxblk][4 rowblocks][slice 0: PP x 16 B | slice 1: PP x 16 B |
+  // slice 2: PP x 8 B] -- kWideOzRec bytes per (8 rows, feature)
+  int8_t* D;
   int32_t maxblk;          // 32-row blocks of the largest Gram row group
 };
-hipError_t launch_wide_oz_scale(const WideArgs& a, const WideOzArgs& o, int K, hipStream_t s);
+hipError_t launch_wide_oz_scale(const WideArgs& a, const WideOzArgs& o, hipStream_t s);
 hipError_t launch_wide_oz_digits(const WideArgs& a, const WideOzArgs& o, bool standardize,
                                  hipStream_t s);
 hipError_t launch_wide_oz_gram(const WideArgs& a, const WideOzArgs& o, hipStream_t s);
 constexpr int kWideOzMaxRows = 32767;  // int32 level sums of one row group
+constexpr int kWideOzRec = 40;         // digit bytes per (8 rows, feature): 5 planes
+// bytes of the digit records of a Gram plan with n_gchunks row groups of at
+// most max_rows rows and PP padded features
+inline int64_t wide_oz_digit_bytes(int n_gchunks, int max_rows, int PP) {
+  const int64_t maxblk = (max_rows + 31) / 32;
+  return (int64_t)(n_gchunks > 1 ? n_gchunks : 1) * maxblk * 4 * PP * kWideOzRec;
+}
 
 // Categorical-code pass (cat_pass.hip): q numeric fp64 columns + F uint8
 // level codes per row; the one-hot blocks of X^T W X are LDS histograms.
@@ -304,6 +322,10 @@ hipError_t launch_level_reset(int K, int P, int start_phase, int32_t* phase, int
                               int32_t* counters, hipStream_t s);
 hipError_t launch_polish_mark(int K, int32_t* phase, const int32_t* status, int32_t* counters,
                               hipStream_t s);
+// theta_rec[k] = theta[k] for the partitions in phase `ph` (before a pass
+// that records the Ozaki digit scales)
+hipError_t launch_theta_snapshot(int K, int P, const int32_t* phase, int ph, const double* theta,
+                                 double* theta_rec, hipStream_t s);
 hipError_t launch_fit_finalize(int K, int P, const double* theta, const double* sig_inv,
                                double* sig_inv_theta, int32_t* status, hipStream_t s);
 hipError_t launch_reduce_partitions(const double* sig_inv, const double* sig_inv_theta,

@@ -264,9 +264,10 @@ __device__ __forceinline__ void store_tiles(Acc (&acc)[(CG<NT, W>::TPW)], double
   });
 }
 
-// CM: also record the chunk's per-feature max |x| into a.colmax (the first
+// CM: also record the chunk's per-feature max |x| into a.colmax and max |z|
+// (z = sqrt(w) x, the fp32 value of the bf16 image) into a.zcolmax (every
 // full-data bf16 pass of a fit; the Ozaki exact pass takes its digit scales
-// from it)
+// from the last record, irls_oz_impl.hpp)
 template <int NT, int W, int PREC, bool STD, int FAM, bool CM = false>
 __global__ __launch_bounds__(64 * W, (W == 8 || NT < 8) ? 2 : 1)
 void irls_coop_kernel(const PassArgs a) {
@@ -325,8 +326,12 @@ void irls_coop_kernel(const PassArgs a) {
   // max is an upper bound over the chunk's rows, which is all the digit
   // exponents need (a looser bound only moves the digits down a bit).
   double cmx[CM ? M : 1];
+  float zmx[CM ? M : 1];  // running max |z| (fp32 image values; rows past the end have w = 0)
 #pragma unroll
-  for (int m = 0; m < (CM ? M : 1); ++m) cmx[m] = 0.0;
+  for (int m = 0; m < (CM ? M : 1); ++m) {
+    cmx[m] = 0.0;
+    zmx[m] = 0.0f;
+  }
   int tI[G::TPW], tJ[G::TPW];  // this wave's tiles (bf16 path)
 #pragma unroll
   for (int i = 0; i < G::TPW; ++i) {
@@ -457,6 +462,10 @@ void irls_coop_kernel(const PassArgs a) {
           // conversion with round-to-odd fix-ups
           asm volatile("" : "+v"(z0), "+v"(z1));
           const f2c pr = {z0 * swf, z1 * swf};
+          if constexpr (CM) {
+            zmx[m] = __builtin_fmaxf(zmx[m], __builtin_fabsf(pr[0]));
+            if (m + 1 < M) zmx[m + 1] = __builtin_fmaxf(zmx[m + 1], __builtin_fabsf(pr[1]));
+          }
           const bf16x2c pk = __builtin_convertvector(pr, bf16x2c);
           obx[(sl + LPR * m) * G::OBS + rB] = pk[0];
           if (m + 1 < M) obx[(sl + LPR * (m + 1)) * G::OBS + rB] = pk[1];
@@ -525,20 +534,31 @@ void irls_coop_kernel(const PassArgs a) {
   }
   if constexpr (CM) {
     __syncthreads();  // red is reused
-    uint32_t* cred = (uint32_t*)smem;  // [W][PMAX]
+    uint32_t* cred = (uint32_t*)smem;  // [2][W][PMAX]: max |x| high dwords, max |z| fp32 bits
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       uint32_t v = __double2hiint(cmx[m]) & 0x7FFFFFFFu;
+      uint32_t u = __float_as_uint(zmx[m]) & 0x7FFFFFFFu;  // non-negative: ordered as integers
 #pragma unroll
-      for (int o = 1; o < RPW; o <<= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
-      if (lane % RPW == 0) cred[wid * G::PMAX + sl + LPR * m] = v;
+      for (int o = 1; o < RPW; o <<= 1) {
+        v = max(v, (uint32_t)__shfl_xor((int)v, o));
+        u = max(u, (uint32_t)__shfl_xor((int)u, o));
+      }
+      if (lane % RPW == 0) {
+        cred[wid * G::PMAX + sl + LPR * m] = v;
+        cred[(W + wid) * G::PMAX + sl + LPR * m] = u;
+      }
     }
     __syncthreads();
     for (int f = tid; f < G::PMAX; f += 64 * W) {
-      uint32_t v = 0;
+      uint32_t v = 0, u = 0;
 #pragma unroll
-      for (int w = 0; w < W; ++w) v = max(v, cred[w * G::PMAX + f]);
+      for (int w = 0; w < W; ++w) {
+        v = max(v, cred[w * G::PMAX + f]);
+        u = max(u, cred[(W + w) * G::PMAX + f]);
+      }
       a.colmax[(int64_t)chunk * G::PMAX + f] = v;
+      a.zcolmax[(int64_t)chunk * G::PMAX + f] = u;
     }
   }
 }

@@ -11,7 +11,7 @@ bool oz_applies(int NT, int p) { return NT >= 1 && NT <= kOzMaxNT && ozk::fits(N
 
 hipError_t launch_irls_oz(const PassArgs& a, int NT, bool standardize, int family, int n_chunks,
                           hipStream_t s) {
-  if (!oz_applies(NT, a.p) || !a.colmax) return hipErrorInvalidValue;
+  if (!oz_applies(NT, a.p) || !a.colmax || !a.zcolmax || !a.theta_rec) return hipErrorInvalidValue;
   switch (NT) {
     case 1: return launch_oz_nt<1>(a, standardize, family, n_chunks, s);
     case 2: return launch_oz_nt<2>(a, standardize, family, n_chunks, s);

@@ -14,8 +14,11 @@
 //
 // Numerics.  z = sqrt(w) x (the fp64 row weight times the
 // fp64 feature).  Per chunk and feature f an exponent E_f with |z_f| < 2^E_f
-// for every row of the chunk, from the chunk's max |x_f| that the fit's first
-// full-data bf16 pass recorded (PassArgs::colmax; sqrt(w) <= 1/2).
+// for every row of the chunk (digit_exponent below): from the max |z_f| that
+// the partition's last full-data bf16 pass recorded at theta_rec
+// (PassArgs::zcolmax), grown by exp(|theta - theta_rec|_1 max|x| / 2), the
+// most sqrt(w) can grow between the two points (|d log sqrt(w) / d eta| <=
+// 1/2), and never above max |x_f| / 2 (sqrt(w) <= 1/2 at every theta).
 // F = round(z 2^(38 - E_f)), |F| < 2^38, by ONE fp64 FMA against
 // 1.5 2^52 + B (B = 0x8080808080): the low 40 mantissa bits of the result are
 // F + B, whose five bytes XOR 0x80 are the balanced signed digits d_0 (most
@@ -213,12 +216,27 @@ __device__ __forceinline__ double level_value(const oz_i4 (&L)[NL], int r) {
   return v;
 }
 
-// digit exponent of a feature from its recorded max |x| high dword: the
-// bound with the low dword all ones, times 1/2 (sqrt(w) <= 1/2) for the
-// logistic family
-__device__ __forceinline__ int digit_exponent(uint32_t hi, int fam_logistic) {
-  const double bound = __hiloint2double((int)(hi & 0x7FFFFFFFu), (int)0xFFFFFFFFu);
-  int e = __builtin_amdgcn_frexp_exp(bound) - fam_logistic;
+// Upper bound of |x| from a recorded max |x| high dword (low dword all ones).
+__device__ __forceinline__ double xbound(uint32_t hi) {
+  return __hiloint2double((int)(hi & 0x7FFFFFFFu), (int)0xFFFFFFFFu);
+}
+// Digit exponent E (bound < 2^E) of a feature of a chunk.  xhi: recorded max
+// |x| high dword; logistic: zbits = recorded max |z| (fp32 bits, z32 =
+// fl32(fl32(x) sqrtf(fl32(w))), within 5 fp32 ulp of z wherever |z| >= 2^-120
+// and w is an fp32 normal), growth = exp(dB / 2) >= the factor sqrt(w) can
+// have grown by since the record.  Rows the fp32 record cannot see have
+// |z| < 2^-120 or sqrt(w) < 2^-60 (w below the fp32 normals), hence the two
+// floors; and sqrt(w) <= 1/2 always.  Gaussian: z = x.
+__device__ __forceinline__ int digit_exponent(uint32_t xhi, uint32_t zbits, double growth,
+                                              int fam_logistic) {
+  const double xb = xbound(xhi);
+  double bound = xb;
+  if (fam_logistic) {
+    const double zb = (double)__uint_as_float(zbits & 0x7FFFFFFFu) * (1.0 + 0x1p-16);
+    bound = fmax(fmax(zb, 0x1p-120), xb * 0x1p-60) * growth;
+    bound = fmin(bound, 0.5 * xb);  // (also when growth overflowed to inf)
+  }
+  const int e = __builtin_amdgcn_frexp_exp(bound);
   return min(max(e, EMIN), EMAX);
 }
 
@@ -392,15 +410,47 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
   double* stdv = bet + PMAX;                        // [2][PMAX] center, 1/scale
   int* ex = (int*)(stdv + 2 * PMAX);                // [PMAX] digit exponents E_f
 
-  for (int f = tid; f < PMAX; f += 64 * (NPW + NCW)) {
-    bet[f] = (f < P) ? a.theta[(int64_t)part * P + f] : 0.0;
-    ex[f] = digit_exponent(a.colmax[(int64_t)chunk * PMAX + f], FAM == FAMILY_LOGISTIC);
+  // digit scales: |theta - theta_rec|_1 and the chunk's max |x| over all
+  // features (PMAX <= 112 < the 512 threads: one feature per thread), reduced
+  // in a fixed order, so every thread forms the same growth factor
+  double dth = 0.0;
+  uint32_t xh = 0;
+  if (tid < PMAX) {
+    const double th = (tid < P) ? a.theta[(int64_t)part * P + tid] : 0.0;
+    bet[tid] = th;
+    if (tid < P) dth = fabs(th - a.theta_rec[(int64_t)part * P + tid]);
+    xh = a.colmax[(int64_t)chunk * PMAX + tid] & 0x7FFFFFFFu;
     if constexpr (STD) {
-      const int j = f - ic;
+      const int j = tid - ic;
       const bool in = j >= 0 && j < p;
-      stdv[f] = in ? a.center[j] : 0.0;
-      stdv[PMAX + f] = in ? 1.0 / a.scale[j] : 1.0;
+      stdv[tid] = in ? a.center[j] : 0.0;
+      stdv[PMAX + tid] = in ? 1.0 / a.scale[j] : 1.0;
     }
+  }
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    dth += __shfl_xor(dth, o);
+    xh = max(xh, (uint32_t)__shfl_xor((int)xh, o));
+  }
+  double* dred = (double*)smem;  // the ring's first bytes, before any DMA
+  uint32_t* xred = (uint32_t*)(dred + (NPW + NCW));
+  if (lane == 0) {
+    dred[wid] = dth;
+    xred[wid] = xh;
+  }
+  __syncthreads();
+  if (tid < PMAX) {
+    double sd = 0.0;
+    uint32_t xm = 0;
+#pragma unroll
+    for (int w = 0; w < NPW + NCW; ++w) {
+      sd += dred[w];
+      xm = max(xm, xred[w]);
+    }
+    const double growth = exp(0.5 * sd * ozk::xbound(xm)) * (1.0 + 0x1p-40);
+    ex[tid] = digit_exponent(a.colmax[(int64_t)chunk * PMAX + tid],
+                             a.zcolmax[(int64_t)chunk * PMAX + tid], growth,
+                             FAM == FAMILY_LOGISTIC);
   }
   // (the ring needs no zeroing: past-the-chunk rows are zeroed in registers
   // and nothing reads a slot's bytes that the DMA did not write)

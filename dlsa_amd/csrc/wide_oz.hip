@@ -8,7 +8,10 @@
 //
 //   wide_row_kernel      (wide_pass.hip) also records per row chunk the max
 //                        |z| = |sqrt(w) x| of every feature (WideArgs::slab_zmax)
-//   wide_oz_scale_kernel per partition and feature E_f with |z| < 2^E_f
+//   wide_oz_scale_kernel per Gram row group and feature E_f with |z| < 2^E_f
+//                        (max over the row chunks that overlap the group: a
+//                        large |z| in one row group does not coarsen the grid
+//                        of the partition's other row groups)
 //   wide_oz_digits_kernel  F = round(z 2^(38 - E_f)) by one FMA against
 //                        1.5 2^52 + 0x8080808080; its five bytes XOR 0x80 are
 //                        balanced digits d_0 .. d_4 (byte r of plane d = digit
@@ -32,7 +35,7 @@ namespace dlsa {
 
 namespace {
 
-constexpr int kRec = 40;               // digit bytes per (8 rows, feature): 5 planes
+constexpr int kRec = kWideOzRec;       // digit bytes per (8 rows, feature): 5 planes
 constexpr int kOzGT = 128;             // output tile edge
 constexpr int kOzStages = 3;           // LDS ring: 2 steps in flight + 1 computed
 constexpr int kPanel = 4 * kOzGT * kRec;  // one panel of a step: 4 rowblocks x 128 features (20 KB)
@@ -40,18 +43,26 @@ constexpr int kPieces = kPanel / 1024;    // 1-KB DMA pieces of a panel (20)
 
 }  // namespace
 
-// E[k, f] from the max over the partition's row chunks (|z| < 2^E: the bound
-// with the low dword all ones)
+// E[g, f] for Gram row group g from the max over the row chunks of its
+// partition whose rows overlap it (|z| < 2^E: the bound with the low dword all
+// ones).  The row chunks of a partition are consecutive and ascending.
 __global__ __launch_bounds__(256) void wide_oz_scale_kernel(const WideArgs a, const WideOzArgs o,
                                                             int PP) {
-  const int k = blockIdx.x;
-  const int c0 = o.rcb[k], c1 = o.rcb[k + 1];
+  const int g = blockIdx.x;
+  const int part = a.gc_part[g];
+  const int64_t r0 = a.gc_row0[g], r1 = r0 + a.gc_rows[g];
+  const int c0 = o.rcb[part], c1 = o.rcb[part + 1];
   for (int f = threadIdx.x; f < PP; f += 256) {
     uint32_t m = 0;
-    for (int c = c0; c < c1; ++c) m = max(m, o.zmax[(int64_t)c * PP + f]);
+    for (int c = c0; c < c1; ++c) {
+      const int64_t s0 = a.rc_row0[c], s1 = s0 + a.rc_rows[c];
+      if (s1 <= r0) continue;
+      if (s0 >= r1) break;
+      m = max(m, o.zmax[(int64_t)c * PP + f]);
+    }
     const double bound = __hiloint2double((int)(m & 0x7FFFFFFFu), (int)0xFFFFFFFFu);
     int e = __builtin_amdgcn_frexp_exp(bound);
-    o.E[(int64_t)k * PP + f] = min(max(e, ozk::EMIN), ozk::EMAX);
+    o.E[(int64_t)g * PP + f] = min(max(e, ozk::EMIN), ozk::EMAX);
   }
 }
 
@@ -77,7 +88,7 @@ __global__ __launch_bounds__(256) void wide_oz_digits_kernel(const WideArgs a, c
   for (int m = 0; m < MB; ++m) {
     const int f = lane + 64 * m, j = f - ic;
     const bool inb = j >= 0 && j < p;
-    const double sc = __builtin_amdgcn_ldexp(1.0, 38 - o.E[(int64_t)part * PP + f]);
+    const double sc = __builtin_amdgcn_ldexp(1.0, 38 - o.E[(int64_t)g * PP + f]);
     double cen = 0.0, isc = 1.0;
     if constexpr (STD) {
       if (inb) {
@@ -145,8 +156,9 @@ __global__ __launch_bounds__(512, 1) void wide_oz_gram_kernel(const WideArgs a, 
   const bool idle = I == J && 32 * qj >= 64 * qi + 64;
   const int nrows = __builtin_amdgcn_readfirstlane(a.gc_rows[g]);
   const int nsteps = (nrows + 31) / 32;
-  // the row group's records: [maxblk][4][PP][48]; a step's panel for
-  // rowblock j is the 6 KB at feature 128 I (A) / 128 J (B)
+  // the row group's records: [maxblk][4 rowblocks][slice 0 (PP x 16 B) | slice 1
+  // (PP x 16 B) | slice 2 (PP x 8 B)]; a step's panel for rowblock j is the
+  // 5 KB of features 128 I .. 128 I + 127 (A) / 128 J .. (B) of its 3 slices
   const uintptr_t gbase = (uintptr_t)(o.D + (int64_t)g * o.maxblk * 4 * PP * kRec);
   const __amdgpu_buffer_rsrc_t dr =
       wv_rsrc(gbase, (uintptr_t)o.maxblk * 4 * PP * kRec);
@@ -239,7 +251,7 @@ __global__ __launch_bounds__(512, 1) void wide_oz_gram_kernel(const WideArgs a, 
   if (idle) return;
   // C/D map of the i32 16x16 MFMA: row 4 (l >> 4) + r, column l & 15
   double* G = a.slab_G + ((int64_t)g * TB + t) * (kOzGT * kOzGT);
-  const int* E = o.E + (int64_t)part * PP;
+  const int* E = o.E + (int64_t)g * PP;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int jl = 32 * qj + 16 * u + fi;
@@ -255,9 +267,9 @@ __global__ __launch_bounds__(512, 1) void wide_oz_gram_kernel(const WideArgs a, 
   }
 }
 
-hipError_t launch_wide_oz_scale(const WideArgs& a, const WideOzArgs& o, int K, hipStream_t s) {
-  if (K <= 0) return hipSuccess;
-  hipLaunchKernelGGL(wide_oz_scale_kernel, dim3(K), dim3(256), 0, s, a, o, kOzGT * a.NB);
+hipError_t launch_wide_oz_scale(const WideArgs& a, const WideOzArgs& o, hipStream_t s) {
+  if (a.n_gchunks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(wide_oz_scale_kernel, dim3(a.n_gchunks), dim3(256), 0, s, a, o, kOzGT * a.NB);
   return hipGetLastError();
 }
 

@@ -20,10 +20,12 @@ from .dlsa import reduce_partitions_device, split_reduced
 
 def combine(buf, group=None):
     """Sum the per-rank reduced buffers in place (RCCL when the process group
-    backend is "nccl", gloo on CPU tensors).  No-op without a process group."""
+    backend is "nccl", gloo on CPU tensors).  No-op without a process group;
+    with one (even of one rank) the all-reduce runs, so a single-GPU job under
+    ``torch.distributed`` takes the same collective path as the 8-GPU one."""
     import torch.distributed as dist
 
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+    if dist.is_available() and dist.is_initialized():
         if buf.is_cuda and dist.get_backend(group) == "gloo":
             # gloo (CPU test / fallback transport): reduce a host copy
             tmp = buf.cpu()

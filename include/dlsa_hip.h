@@ -123,13 +123,25 @@ typedef struct dlsa_fit_stats {
                                exact pass publishing Sig_inv at their theta */
   int32_t passes_oz;        /* of passes_fp64: on the int8 matrix cores (Ozaki
                                digit slices) */
+  int32_t oz_fallbacks;     /* P > DLSA_MAX_P_FUSED, mixed mode: fits whose exact
+                               Gram took the fp64 MFMA path because the int8
+                               digit records had no room (a workspace of at least
+                               the size without them but smaller than
+                               dlsa_logistic_workspace_bytes, a failed
+                               allocation, or DLSA_WIDE_OZ_MAX_BYTES) */
 } dlsa_fit_stats;
 
 /* Default options (mixed Hessian, automatic chunking, no timing). */
 void dlsa_fit_options_default(dlsa_fit_options* opt);
 
 /* Device scratch needed by a fit with these partitions (offsets: HOST array of
- * K+1 int64).  Pass at least this many bytes in dlsa_fit_options.workspace. */
+ * K+1 int64).  Pass at least this many bytes in dlsa_fit_options.workspace.
+ * For P > DLSA_MAX_P_FUSED this includes the int8 digit records of the
+ * mixed-mode exact Gram (n * PP * 5 bytes, PP = P rounded up to 128; DESIGN.md
+ * 4.4b): a smaller workspace that still holds everything else runs the fp64
+ * Gram instead (dlsa_fit_stats.oz_fallbacks).  The library keeps no device
+ * memory between calls: a NULL workspace is allocated on the stream and
+ * freed before return. */
 int64_t dlsa_logistic_workspace_bytes(const int64_t* offsets, int32_t K,
                                       int32_t p, int32_t fit_intercept,
                                       int32_t rows_per_chunk);

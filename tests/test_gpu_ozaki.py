@@ -1,8 +1,10 @@
 """GPU: the exact pass on the int8 matrix cores (irls_oz_impl.hpp).
 
-In mixed mode the fit's first full-data bf16 pass records every chunk's
-per-feature max |x|, and the exact pass that publishes Sig_inv (models.py:130)
-then forms X^T W X from int8 digit slices with exact int32 sums.  The same fit
+In mixed mode every full-data bf16 pass records, per chunk and feature, max
+|x| and max |sqrt(w) x| at the theta it saw, and the exact pass that publishes
+Sig_inv (models.py:130) then forms X^T W X from int8 digit slices with exact
+int32 sums, its digit exponents from that record (grown by the bound on how
+far sqrt(w) can have moved since).  The same fit
 with DLSA_OZ=0 runs the fp64-MFMA exact pass at the SAME iterate (the bf16
 passes are deterministic), so the two Sig_inv differ only by the Ozaki
 scheme's error: asserted below 1e-11 relative to the largest entry (the
@@ -40,6 +42,49 @@ def torch_cuda():
 def M():
     from dlsa_amd import models
     return models
+
+
+def _elem(a, b):
+    """max_ij |a_ij - b_ij| / sqrt(b_ii b_jj) over partitions [K, P, P]: the
+    per-entry error on the scale of the entry's own rows and columns (a
+    relative-to-the-largest-entry metric cannot see errors in small entries)."""
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    worst = 0.0
+    for k in range(b.shape[0]):
+        d = np.sqrt(np.abs(np.diagonal(b[k])))
+        scale = np.outer(d, d)
+        m = scale > 0
+        worst = max(worst, float((np.abs(a[k] - b[k])[m] / scale[m]).max()))
+    return worst
+
+
+def heavy_design(kind, n, chunk=4096, seed=0, p_extra=0):
+    """Designs where one digit exponent per chunk column is weakest:
+    lognormal: a lognormal(0, 2) column (max/median ~ 1e3);
+    outlier: a U(-1/2, 1/2) column with one 1e4 entry per `chunk` rows, whose
+      coefficient 0.8 makes eta ~ 8000 there (w = 0: the row's z is 0 while
+      its |x| is 2e4 times the column's others);
+    separable: |eta| ~ N(0, 12^2) (median 7.6, most rows |eta| < 20: weights
+      down to e^-20).
+    p_extra U(-1/2, 1/2) columns with zero coefficients are appended."""
+    rs = np.random.RandomState(seed)
+    if kind == "lognormal":
+        X = np.column_stack([rs.randn(n, 6), rs.lognormal(0.0, 2.0, n)])
+        beta = np.array([0.5, -0.4, 0.3, 0.2, -0.1, 0.3, 0.05])
+    elif kind == "outlier":
+        c = rs.rand(n) - 0.5
+        c[chunk // 2::chunk] = 1e4
+        X = np.column_stack([rs.randn(n, 6), c])
+        beta = np.array([0.5, -0.4, 0.3, 0.2, -0.1, 0.3, 0.8])
+    else:
+        X = rs.randn(n, 6)
+        beta = np.array([6.0, -5.0, 4.0, 5.0, -3.0, 4.0])
+    eta = X @ beta
+    y = (rs.rand(n) < 1.0 / (1.0 + np.exp(-eta))).astype(np.float64)
+    if p_extra:
+        X = np.column_stack([X, rs.rand(n, p_extra) - 0.5])
+    return X, y
 
 
 def _pair(M, monkeypatch, *args, **kw):
@@ -167,3 +212,195 @@ def test_wide_ozaki_gram_matches_fp64_gram(torch_cuda, M, monkeypatch, p, fi, st
     assert _rel(oz.theta.cpu(), th) < REL
     assert _rel(oz.sig_inv.cpu(), S) < REL
     assert _rel(oz.sig_inv_theta.cpu(), St) < REL
+
+
+ELEM = 1e-10
+
+
+@pytest.mark.parametrize("kind", ["lognormal", "outlier", "separable"])
+@pytest.mark.parametrize("p_extra", [0, 93])
+def test_ozaki_heavy_tails_per_entry(torch_cuda, M, monkeypatch, kind, p_extra):
+    """Default mode, fused int8 exact pass (P = 8 and P = 101, NT 1 and 7):
+    the designs of heavy_design against the fp64 exact pass at the same
+    iterate and against the oracle, entry by entry: max |dH_ij| / sqrt(H_ii
+    H_jj) < 1e-10, theta within 1e-8.  (Digit exponents from the chunk's max
+    |x| / 2 -- the round-3 rule -- miss this by 5 orders of magnitude on the
+    outlier column, tests/test_cpu_ozaki_numerics.py.)"""
+    n, chunk = 40000, 4096
+    X, y = heavy_design(kind, n, chunk=chunk, p_extra=p_extra)
+    off = np.array([0, 20000, n])
+    oz, f64 = _pair(M, monkeypatch, X, y, off, fit_intercept=True, rows_per_chunk=chunk)
+    assert oz.stats["passes_oz"] >= 1 and f64.stats["passes_oz"] == 0
+    assert (oz.status.cpu().numpy() == 0).all()
+    assert _elem(oz.sig_inv.cpu(), f64.sig_inv.cpu()) < ELEM
+    assert _rel(oz.theta.cpu(), f64.theta.cpu()) < 1e-12
+    th, S, St, _, _ = O.logistic_fit_partitions(X, y, off, fit_intercept=True)
+    assert _rel(oz.theta.cpu(), th) < REL
+    assert _elem(oz.sig_inv.cpu(), S) < ELEM
+    assert _rel(oz.sig_inv_theta.cpu(), St) < REL
+
+
+@pytest.mark.parametrize("kind", ["lognormal", "outlier", "separable"])
+def test_wide_ozaki_heavy_tails_per_entry(torch_cuda, M, monkeypatch, kind):
+    """The same designs on the wide path (P = 208: row pass + int8 Gram with
+    per-row-group digit exponents, wide_oz.hip)."""
+    n, chunk = 24000, 4096
+    X, y = heavy_design(kind, n, chunk=chunk, p_extra=200)
+    off = np.array([0, 12000, n])
+    oz, f64 = _pair(M, monkeypatch, X, y, off, fit_intercept=True, rows_per_chunk=chunk)
+    assert oz.stats["passes_oz"] >= 1 and f64.stats["passes_oz"] == 0
+    assert (oz.status.cpu().numpy() == 0).all()
+    assert _elem(oz.sig_inv.cpu(), f64.sig_inv.cpu()) < ELEM
+    assert _rel(oz.theta.cpu(), f64.theta.cpu()) < 1e-12
+    th, S, _, _, _ = O.logistic_fit_partitions(X, y, off, fit_intercept=True)
+    assert _rel(oz.theta.cpu(), th) < REL
+    assert _elem(oz.sig_inv.cpu(), S) < ELEM
+
+
+def _wide_problem(p, seed):
+    sizes = [6000, 5001, 4000]
+    X, y = O.simulate_counter(sum(sizes), p, seed=seed)
+    return X, y, np.concatenate([[0], np.cumsum(sizes)])
+
+
+def test_wide_ozaki_concurrent_fits_two_threads(torch_cuda, M):
+    """Two wide mixed-mode fits (P = 300, then the larger P = 500) on two Python
+    threads, each on its own torch stream: the digit records live in each
+    fit's own workspace (no process-wide buffer), so both equal the sequential
+    fits bit for bit, with the int8 Gram used in both."""
+    import threading
+
+    torch = torch_cuda
+    probs = {p: _wide_problem(p, 40 + p) for p in (300, 500)}
+    seq = {}
+    for p, (X, y, off) in probs.items():
+        seq[p] = M.logistic_model_batched(X, y, off, rows_per_chunk=2000)
+        assert seq[p].stats["passes_oz"] >= 1
+    Xd = {p: (torch.from_numpy(X).cuda(), torch.from_numpy(y).cuda()) for p, (X, y, _) in
+          probs.items()}
+    torch.cuda.synchronize()
+    out, err = {}, []
+    go = threading.Barrier(2)
+
+    def run(p):
+        try:
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                go.wait()
+                f = M.logistic_model_batched(Xd[p][0], Xd[p][1], probs[p][2],
+                                             rows_per_chunk=2000)
+                s.synchronize()
+                out[p] = f
+        except Exception as e:  # pragma: no cover - reported below
+            err.append(e)
+
+    ts = [threading.Thread(target=run, args=(p,)) for p in (300, 500)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not err, err
+    for p in (300, 500):
+        assert out[p].stats["passes_oz"] >= 1
+        assert torch.equal(out[p].theta, seq[p].theta)
+        assert torch.equal(out[p].sig_inv, seq[p].sig_inv)
+        assert torch.equal(out[p].loglik, seq[p].loglik)
+
+
+def _abi_fit(torch, X, y, off, p, workspace_bytes, guard=0, pattern=0xA5, rows_per_chunk=2000):
+    """dlsa_logistic_fit_batched_ex through ctypes with a caller workspace of
+    exactly `workspace_bytes` (plus `guard` bytes of `pattern` after it, or a
+    NULL workspace when workspace_bytes is None)."""
+    import ctypes
+
+    from dlsa_amd import _hip
+
+    lib = _hip.load()
+    K = len(off) - 1
+    Xd = torch.from_numpy(np.ascontiguousarray(X)).cuda()
+    yd = torch.from_numpy(np.ascontiguousarray(y)).cuda()
+    th = torch.empty(K, p, dtype=torch.float64, device="cuda")
+    S = torch.empty(K, p, p, dtype=torch.float64, device="cuda")
+    St = torch.empty(K, p, dtype=torch.float64, device="cuda")
+    ll = torch.empty(K, dtype=torch.float64, device="cuda")
+    it = torch.empty(K, dtype=torch.int32, device="cuda")
+    st = torch.empty(K, dtype=torch.int32, device="cuda")
+    opt = _hip.default_options()
+    opt.rows_per_chunk = rows_per_chunk
+    ws = None
+    if workspace_bytes is not None:
+        ws = torch.full((workspace_bytes + guard,), pattern, dtype=torch.uint8, device="cuda")
+        opt.workspace = ws.data_ptr()
+        opt.workspace_bytes = workspace_bytes
+    offs = np.ascontiguousarray(off, dtype=np.int64)
+    rc = lib.dlsa_logistic_fit_batched_ex(
+        Xd.data_ptr(), yd.data_ptr(), offs.ctypes.data_as(ctypes.c_void_p), K, p, 0, None, None,
+        100, 1e-10, th.data_ptr(), S.data_ptr(), St.data_ptr(), ll.data_ptr(), it.data_ptr(),
+        st.data_ptr(), ctypes.byref(opt), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    _hip.check(rc, "dlsa_logistic_fit_batched_ex")
+    return th.cpu(), S.cpu(), _hip.last_fit_stats(), ws
+
+
+def test_wide_ozaki_workspace_ownership_and_fallback(torch_cuda, M, monkeypatch):
+    """The digit records are part of the workspace dlsa_logistic_workspace_bytes
+    reports.  A workspace of exactly that size runs the int8 Gram and writes
+    nothing past its end (a guard band of 1 MiB keeps its fill pattern); one
+    byte less cannot hold the records and runs the fp64 Gram (oz_fallbacks =
+    1, no error); a NULL workspace is allocated and freed inside the call;
+    DLSA_WIDE_OZ_MAX_BYTES below the records' size falls back the same way."""
+    import ctypes
+
+    torch = torch_cuda
+    from dlsa_amd import _hip
+
+    p = 300
+    X, y, off = _wide_problem(p, 77)
+    lib = _hip.load()
+    offs = np.ascontiguousarray(off, dtype=np.int64)
+    need = lib.dlsa_logistic_workspace_bytes(offs.ctypes.data_as(ctypes.c_void_p), len(off) - 1,
+                                             p, 0, 2000)
+    assert need > 0
+    guard = 1 << 20
+    th, S, st, ws = _abi_fit(torch, X, y, off, p, need, guard=guard)
+    assert st["passes_oz"] >= 1 and st["oz_fallbacks"] == 0
+    tail = ws[need:].cpu().numpy()
+    assert (tail == 0xA5).all(), "the fit wrote past the end of its workspace"
+    th_f, S_f, st_f, _ = _abi_fit(torch, X, y, off, p, need - 1)
+    assert st_f["passes_oz"] == 0 and st_f["oz_fallbacks"] == 1
+    th_n, S_n, st_n, _ = _abi_fit(torch, X, y, off, p, None)
+    assert st_n["passes_oz"] >= 1 and st_n["oz_fallbacks"] == 0
+    assert torch.equal(th_n, th) and torch.equal(S_n, S)
+    monkeypatch.setenv("DLSA_WIDE_OZ_MAX_BYTES", "4096")
+    th_c, S_c, st_c, _ = _abi_fit(torch, X, y, off, p, need)
+    monkeypatch.delenv("DLSA_WIDE_OZ_MAX_BYTES")
+    assert st_c["passes_oz"] == 0 and st_c["oz_fallbacks"] == 1
+    assert torch.equal(th_c, th_f) and torch.equal(S_c, S_f)
+    thr, Sr, _, _, _ = O.logistic_fit_partitions(X, y, off)
+    for t_, s_ in ((th, S), (th_f, S_f)):
+        assert _rel(t_, thr) < REL
+        assert _rel(s_, Sr) < REL
+    assert _elem(S, S_f) < ELEM
+
+
+@pytest.mark.parametrize("p,rows", [(201, 2000), (300, 1000), (500, 4096), (384, 32767)])
+def test_wide_ozaki_digit_records_stay_in_bounds(torch_cuda, M, p, rows):
+    """Ragged row groups (partial 32-row blocks, groups of 1 .. 32767 rows,
+    PP = 256 / 384 / 512) with a 1 MiB guard band after the workspace: the
+    digits kernel's records and every other workspace region stay inside it,
+    and the fit matches the oracle."""
+    torch = torch_cuda
+    sizes = [rows + 17, 3, 1001, 40] if rows < 32767 else [32767, 5]
+    X, y = O.simulate_counter(sum(sizes), p, seed=p + rows)
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    import ctypes
+
+    from dlsa_amd import _hip
+
+    lib = _hip.load()
+    offs = np.ascontiguousarray(off, dtype=np.int64)
+    need = lib.dlsa_logistic_workspace_bytes(offs.ctypes.data_as(ctypes.c_void_p), len(off) - 1,
+                                             p, 0, rows)
+    th, S, st, ws = _abi_fit(torch, X, y, off, p, need, guard=1 << 20, rows_per_chunk=rows)
+    assert st["passes_oz"] >= 1
+    assert (ws[need:].cpu().numpy() == 0xA5).all()

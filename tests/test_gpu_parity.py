@@ -455,33 +455,41 @@ def test_wide_ols_vs_oracle(torch_cuda, M, p, fi):
 
 
 def test_config5_shape_sampled_partitions(torch_cuda, M):
-    """BASELINE config-5 partition geometry (p = 500, n_k = 156 250) on 8
-    partitions generated in HBM: 1 sampled partition against the oracle, every
+    """BASELINE config 5 exactly (p = 500, n = 5e6, K = 32 partitions of
+    156 250 rows generated in HBM, the default mixed fit: bf16 fused passes +
+    the int8 exact Gram): partitions 0 and 31 against the oracle, every
     partition through the score equation X^T (y - mu) ~ 0 and Sig_inv
-    symmetry; then the combine + DBIC selection on the 8 partitions."""
+    symmetry; then the combine, whose DBIC support must EQUAL the oracle's
+    selection on the same sums (dlsa/dlsa.py:70-100)."""
     torch = torch_cuda
     from dlsa_amd.dlsa import dlsa, dlsa_mapred
 
-    K, nk, p = 8, 156250, 500
+    K, nk, p = 32, 156250, 500
     X, y = M.simulate_logistic_device(K * nk, p, seed=2019)
     off = np.arange(K + 1, dtype=np.int64) * nk
     fit = M.logistic_model_batched(X, y, off)
     assert (fit.status.cpu().numpy() == 0).all()
+    assert fit.stats["passes_oz"] >= 1
     S = fit.sig_inv
     assert torch.equal(S, S.transpose(1, 2))
-    k = 5
-    o = O.logistic_fit(X[off[k]:off[k + 1]].cpu().numpy(), y[off[k]:off[k + 1]].cpu().numpy())
-    assert _rel(fit.theta[k].cpu(), o["coef"]) < REL
-    assert _rel(fit.sig_inv[k].cpu(), o["Sig_inv"]) < REL
+    for k in (0, K - 1):
+        o = O.logistic_fit(X[off[k]:off[k + 1]].cpu().numpy(),
+                           y[off[k]:off[k + 1]].cpu().numpy())
+        assert _rel(fit.theta[k].cpu(), o["coef"]) < REL
+        assert _rel(fit.sig_inv[k].cpu(), o["Sig_inv"]) < REL
+        assert _rel(fit.sig_inv_theta[k].cpu(), o["Sig_invMcoef"]) < REL
     th = fit.theta
     for k in range(K):
         Xk = X[off[k]:off[k + 1]]
         gk = Xk.T @ (y[off[k]:off[k + 1]] - torch.sigmoid(Xk @ th[k]))
         assert gk.abs().max().item() < 1e-5
     comb = dlsa_mapred(fit)
-    sel = dlsa(comb.iloc[:, 2:], comb["beta_byOLS"], K * nk)
-    sup = set(np.nonzero(sel["beta_byBIC"].to_numpy())[0].tolist())
-    assert set(range(200)) <= sup  # the 0.4 p true nonzeros are all kept
+    Ssum = comb.iloc[:, 2:].to_numpy()
+    sel = dlsa(Ssum, comb["beta_byOLS"], K * nk)
+    _, b_bic = O.dlsa(Ssum, comb["beta_byOLS"].to_numpy(), K * nk)
+    sup = np.nonzero(sel["beta_byBIC"].to_numpy())[0].tolist()
+    assert sup == np.nonzero(b_bic)[0].tolist()
+    assert set(range(200)) <= set(sup)  # the 0.4 p true nonzeros are all kept
 
 
 # ---------------------------------------------------------------------------

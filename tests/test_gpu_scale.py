@@ -28,6 +28,14 @@ def _rel(a, b):
     return np.abs(a - b).max() / max(np.abs(b).max(), 1e-300)
 
 
+def _elem(a, b):
+    """max_ij |a_ij - b_ij| / sqrt(b_ii b_jj): every entry on its own scale."""
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    d = np.sqrt(np.abs(np.diagonal(b)))
+    return float((np.abs(a - b) / np.outer(d, d)).max())
+
+
 @pytest.fixture(scope="module")
 def torch_cuda():
     import torch
@@ -72,7 +80,9 @@ def test_config2_full_K1024(torch_cuda, M):
         o = O.logistic_fit(X[a:b].cpu().numpy(), y[a:b].cpu().numpy())
         assert _rel(fit.theta[k].cpu(), o["coef"]) < REL
         assert _rel(fit.sig_inv[k].cpu(), o["Sig_inv"]) < REL
+        assert _elem(fit.sig_inv[k].cpu(), o["Sig_inv"]) < 1e-10  # the int8 exact pass, per entry
         assert _rel(fit.sig_inv_theta[k].cpu(), o["Sig_invMcoef"]) < REL
+    assert fit.stats["passes_oz"] >= 1
     comb = dlsa_mapred(fit)
     Ssum = comb.iloc[:, 2:].to_numpy()
     wlse_ref = np.linalg.lstsq(Ssum, fit.sig_inv_theta.sum(0).cpu().numpy(), rcond=None)[0]
