@@ -40,8 +40,27 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()) -> str:
-    """Compile every source to an object in parallel, then link the .so."""
+OBJ_CACHE = os.path.join(ROOT, "build", "obj")
+
+
+def _cached_object(src: str) -> str | None:
+    """The object of `src` from the last product build (no defines), if it is
+    newer than the source and every header."""
+    obj = os.path.join(OBJ_CACHE, os.path.splitext(src)[0] + ".o")
+    if not os.path.exists(obj):
+        return None
+    t = os.path.getmtime(obj)
+    deps = [os.path.join(CSRC, src)] + [os.path.join(CSRC, h) for h in HEADERS] + [__file__]
+    return obj if all(os.path.getmtime(d) <= t for d in deps) else None
+
+
+def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=(),
+          only=None) -> str:
+    """Compile every source to an object in parallel, then link the .so.
+
+    Profiling variants (out != OUT) may name `only`: the sources the defines
+    apply to; the other objects are taken from the product build's object
+    cache (build/obj) when it is current."""
     if not force and out == OUT and not _stale():
         return OUT
     import tempfile
@@ -49,12 +68,20 @@ def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()
 
     common = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
               "-Wall", "-Wno-unused-function", "-Wno-unused-command-line-argument",
-              "-I" + os.path.join(ROOT, "include"), *[f"-D{d}" for d in defines]]
+              "-I" + os.path.join(ROOT, "include")]
+    product = out == OUT and not defines
     jobs = int(os.environ.get("DLSA_BUILD_JOBS", min(8, os.cpu_count() or 1)))
     with tempfile.TemporaryDirectory(prefix="dlsa_build_") as tmp:
         def compile_one(src):
+            # reuse the cached object of a source whose object is current: the
+            # variant builds' untouched sources, and an incremental product build
+            if (only is not None and src not in only) or (product and not force):
+                cached = _cached_object(src)
+                if cached:
+                    return cached, None
             obj = os.path.join(tmp, os.path.splitext(src)[0] + ".o")
-            cmd = common + ["-c", os.path.join(CSRC, src), "-o", obj]
+            cmd = common + ([f"-D{d}" for d in defines] if only is None or src in only else [])
+            cmd = cmd + ["-c", os.path.join(CSRC, src), "-o", obj]
             if src.endswith(".cpp"):  # host-only code (LARS): AVX2/FMA vector loops (x86-64-v3)
                 cmd += ["-march=x86-64-v3"]
             if verbose:
@@ -64,9 +91,14 @@ def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()
         with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
             results = list(ex.map(compile_one, SOURCES))
         for obj, res in results:
-            if res.returncode != 0:
+            if res is not None and res.returncode != 0:
                 sys.stderr.write(res.stdout + res.stderr)
                 raise RuntimeError(f"hipcc failed on {obj} ({res.returncode})")
+        if product:  # keep the objects for variant builds
+            os.makedirs(OBJ_CACHE, exist_ok=True)
+            for obj, res in results:
+                if res is not None:
+                    shutil.copy2(obj, os.path.join(OBJ_CACHE, os.path.basename(obj)))
         cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC",
                *[o for o, _ in results], "-o", out + ".tmp"]
         if verbose:

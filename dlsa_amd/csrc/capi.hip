@@ -1013,10 +1013,12 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
   const bool trace = getenv("DLSA_TRACE") != nullptr;
   int32_t* h_phase = h_cnt + 4;  // [K] phases (pinned: no staging copy per iteration)
   // exact passes on the int8 matrix cores (irls_oz_impl.hpp) unless DLSA_OZ=0:
-  // every full-data bf16 pass records, per chunk and feature, max |x| and max
-  // |sqrt(w) x| at the theta it saw (snapshotted into theta_rec first), and
-  // the exact passes of the final plan take their digit scales from the
-  // partition's last record
+  // the first full-data bf16 pass records, per chunk and feature, max |x|; the
+  // bf16 passes that follow an iteration with a partition near the switch
+  // (counters[3], kOzNearTol) record max |sqrt(w) x| at the theta they saw
+  // (snapshotted into theta_rec first); the exact passes of the final plan
+  // take their digit scales from the partition's last records (a chunk with
+  // no max |z| record -- zcolmax = +inf, theta_rec = 0 -- gets max |x| / 2)
   const bool use_oz = !(getenv("DLSA_OZ") && atoi(getenv("DLSA_OZ")) == 0) &&
                       approx_prec == PREC_BF16 && oz_applies(pl.NT, p) &&
                       pl.max_chunk_rows <= kOzMaxRows;
@@ -1024,6 +1026,14 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
   uint32_t* d_zcolmax = (uint32_t*)at(L.off_zcolmax);
   double* d_threc = (double*)at(L.off_threc);
   bool colmax_ready = false;
+  bool near_switch = false;  // counters[3] of the last solve
+  // DLSA_OZ_ZREC=0 (A/B only): no max |z| records, every exponent from max |x| / 2
+  const bool zrec = !(getenv("DLSA_OZ_ZREC") && atoi(getenv("DLSA_OZ_ZREC")) == 0);
+  if (use_oz) {
+    DLSA_HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)d_zcolmax, 0x7F800000u,
+                                   (size_t)std::max(pl.n_chunks, 1) * pl.PP, stream));
+    DLSA_HIP_TRY(hipMemsetAsync(d_threc, 0, 8LL * K * P, stream));
+  }
   // one pass over the chunks of plan q whose partition is in phase ph:
   // exact (fp64 Hessian) passes by the per-wave kernel up to P = 128 and the
   // cooperative one above; approximate passes (PHASE_F32 at the fit's
@@ -1036,22 +1046,24 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
     pa.want_phase = ph;
     const bool wave = f64 && q.NT <= kWaveMaxNT;
     const bool oz = wave && use_oz && colmax_ready && full;
-    // every full-data bf16 pass records the digit scales
-    const bool record = use_oz && full && ph == PHASE_F32;
-    if (record) {
+    // digit-scale records of a full-data bf16 pass: max |x| on the first,
+    // max |z| near the switch
+    const bool rec_x = use_oz && full && ph == PHASE_F32 && !colmax_ready;
+    const bool rec_z = use_oz && full && ph == PHASE_F32 && near_switch && zrec;
+    if (rec_z) {
       hipError_t e = launch_theta_snapshot(K, P, d_phase, PHASE_F32, theta, d_threc, stream);
       if (e != hipSuccess) return e;
     }
     hipError_t e = timed(f64 ? &g_stats.ms_pass_fp64 : &g_stats.ms_pass_fp32, [&] {
       PassArgs pc = pa;
-      pc.colmax = (oz || record) ? d_colmax : nullptr;
-      pc.zcolmax = (oz || record) ? d_zcolmax : nullptr;
+      pc.colmax = (oz || rec_x) ? d_colmax : nullptr;
+      pc.zcolmax = (oz || rec_z) ? d_zcolmax : nullptr;
       pc.theta_rec = d_threc;
       if (oz) return launch_irls_oz(pc, q.NT, standardize, family, q.n_chunks, stream);
       if (wave) return launch_irls_wave(pc, q.NT, standardize, family, q.n_chunks, stream);
       return launch_irls_coop(pc, q.NT, prec, standardize, family, q.n_chunks, stream);
     });
-    if (record) colmax_ready = true;
+    if (rec_x) colmax_ready = true;
     if (oz) g_stats.passes_oz++;
     if (f64) {
       g_stats.passes_fp64++;
@@ -1101,6 +1113,7 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
       DLSA_HIP_TRY(hipMemcpyAsync(h_phase, d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
       DLSA_HIP_TRY(hipStreamSynchronize(stream));
       for (int ph = 0; ph < kRunPhases; ++ph) n_running[ph] = h_cnt[ph];
+      near_switch = final_level && h_cnt[3] > 0;
       if (trace) DLSA_HIP_TRY(trace_iteration(K, P, theta, d_dprev, lvl, it, n_running));
     }
   }

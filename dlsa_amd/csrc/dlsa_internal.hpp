@@ -91,7 +91,8 @@ struct SolveArgs {
   int32_t* backtracks;  // [K]
   int32_t* iters;       // [K]
   int32_t* status;      // [K]
-  int32_t* counters;    // [kRunPhases] partitions still running per phase
+  int32_t* counters;    // [4]: [kRunPhases] partitions still running per phase, [3] of the
+                        // PHASE_F32 ones, those whose step was <= kOzNearTol (1 + max|theta|)
   double* dm_prev;      // [K] max |step| of the last approximate iteration (0: none)
   int32_t* stall;       // [K] consecutive stalled approximate iterations
   double* sig_inv;      // [K, P, P] out
@@ -119,6 +120,10 @@ struct SolveArgs {
 // backtracks; two stalls in a row move the partition one precision up
 // (F32 -> escalate_to, F32X -> F64).  Returns the phase to continue in.
 constexpr double kStallDll = 1e-5;
+// An approximate iteration whose max |step| is below kOzNearTol (1 + max|theta|)
+// is one or two iterations from the exact pass: the next bf16 pass records
+// max |sqrt(w) x| for the Ozaki digit scales (capi.hip, irls_oz_impl.hpp)
+constexpr double kOzNearTol = 1e-2;
 __device__ __forceinline__ int32_t escalate_phase(const SolveArgs& a, int32_t ph) {
   return ph == PHASE_F32 ? a.escalate_to : PHASE_F64;
 }

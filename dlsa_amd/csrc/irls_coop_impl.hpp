@@ -264,11 +264,12 @@ __device__ __forceinline__ void store_tiles(Acc (&acc)[(CG<NT, W>::TPW)], double
   });
 }
 
-// CM: also record the chunk's per-feature max |x| into a.colmax and max |z|
-// (z = sqrt(w) x, the fp32 value of the bf16 image) into a.zcolmax (every
-// full-data bf16 pass of a fit; the Ozaki exact pass takes its digit scales
-// from the last record, irls_oz_impl.hpp)
-template <int NT, int W, int PREC, bool STD, int FAM, bool CM = false>
+// CM (bits): also record the chunk's per-feature max |x| into a.colmax (1:
+// the fit's first full-data bf16 pass) and max |z| (z = sqrt(w) x, the fp32
+// value of the bf16 image) into a.zcolmax (2: the bf16 passes of partitions
+// near convergence); the Ozaki exact pass takes its digit scales from the
+// last records (irls_oz_impl.hpp)
+template <int NT, int W, int PREC, bool STD, int FAM, int CM = 0>
 __global__ __launch_bounds__(64 * W, (W == 8 || NT < 8) ? 2 : 1)
 void irls_coop_kernel(const PassArgs a) {
   using G = CG<NT, W>;
@@ -325,12 +326,12 @@ void irls_coop_kernel(const PassArgs a) {
   // are the next chunk's rows (or the range check's zeros), so the recorded
   // max is an upper bound over the chunk's rows, which is all the digit
   // exponents need (a looser bound only moves the digits down a bit).
-  double cmx[CM ? M : 1];
-  float zmx[CM ? M : 1];  // running max |z| (fp32 image values; rows past the end have w = 0)
+  double cmx[(CM & 1) ? M : 1];
+  float zmx[(CM & 2) ? M : 1];  // running max |z| (fp32 image values; rows past the end have w = 0)
 #pragma unroll
   for (int m = 0; m < (CM ? M : 1); ++m) {
-    cmx[m] = 0.0;
-    zmx[m] = 0.0f;
+    if constexpr (CM & 1) cmx[m] = 0.0;
+    if constexpr (CM & 2) zmx[m] = 0.0f;
   }
   int tI[G::TPW], tJ[G::TPW];  // this wave's tiles (bf16 path)
 #pragma unroll
@@ -410,7 +411,7 @@ void irls_coop_kernel(const PassArgs a) {
         if constexpr (STD) v = (v - stdv[sl + LPR * m]) * stdv[G::PMAX + sl + LPR * m];
         if (m == 0 && ic && sl == 0) v = 1.0;
         xv[m] = v;
-        if constexpr (CM) asm("v_max_f64 %0, %0, |%1|" : "+v"(cmx[m]) : "v"(v));
+        if constexpr (CM & 1) asm("v_max_f64 %0, %0, |%1|" : "+v"(cmx[m]) : "v"(v));
         if (m & 1)
           e1 = fma(v, beta[m], e1);
         else
@@ -462,7 +463,7 @@ void irls_coop_kernel(const PassArgs a) {
           // conversion with round-to-odd fix-ups
           asm volatile("" : "+v"(z0), "+v"(z1));
           const f2c pr = {z0 * swf, z1 * swf};
-          if constexpr (CM) {
+          if constexpr ((CM & 2) != 0) {
             zmx[m] = __builtin_fmaxf(zmx[m], __builtin_fabsf(pr[0]));
             if (m + 1 < M) zmx[m + 1] = __builtin_fmaxf(zmx[m + 1], __builtin_fabsf(pr[1]));
           }
@@ -537,12 +538,13 @@ void irls_coop_kernel(const PassArgs a) {
     uint32_t* cred = (uint32_t*)smem;  // [2][W][PMAX]: max |x| high dwords, max |z| fp32 bits
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-      uint32_t v = __double2hiint(cmx[m]) & 0x7FFFFFFFu;
-      uint32_t u = __float_as_uint(zmx[m]) & 0x7FFFFFFFu;  // non-negative: ordered as integers
+      uint32_t v = 0, u = 0;
+      if constexpr (CM & 1) v = __double2hiint(cmx[m]) & 0x7FFFFFFFu;
+      if constexpr (CM & 2) u = __float_as_uint(zmx[m]) & 0x7FFFFFFFu;  // ordered as integers
 #pragma unroll
       for (int o = 1; o < RPW; o <<= 1) {
-        v = max(v, (uint32_t)__shfl_xor((int)v, o));
-        u = max(u, (uint32_t)__shfl_xor((int)u, o));
+        if constexpr (CM & 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+        if constexpr (CM & 2) u = max(u, (uint32_t)__shfl_xor((int)u, o));
       }
       if (lane % RPW == 0) {
         cred[wid * G::PMAX + sl + LPR * m] = v;
@@ -557,13 +559,13 @@ void irls_coop_kernel(const PassArgs a) {
         v = max(v, cred[w * G::PMAX + f]);
         u = max(u, cred[(W + w) * G::PMAX + f]);
       }
-      a.colmax[(int64_t)chunk * G::PMAX + f] = v;
-      a.zcolmax[(int64_t)chunk * G::PMAX + f] = u;
+      if constexpr (CM & 1) a.colmax[(int64_t)chunk * G::PMAX + f] = v;
+      if constexpr (CM & 2) a.zcolmax[(int64_t)chunk * G::PMAX + f] = u;
     }
   }
 }
 
-template <int NT, int W, int PREC, bool STD, int FAM, bool CM = false>
+template <int NT, int W, int PREC, bool STD, int FAM, int CM = 0>
 static hipError_t launch_c(const PassArgs& a, int n_chunks, hipStream_t s) {
   auto kern = irls_coop_kernel<NT, W, PREC, STD, FAM, CM>;
   const size_t lds =
@@ -585,9 +587,16 @@ static hipError_t launch_coop_ntw(const PassArgs& a, int prec, bool std_, int fa
   switch (prec) {
     case PREC_BF16:
       if constexpr (NT <= kOzMaxNT) {
-        if (a.colmax)
-          return std_ ? launch_c<NT, W, PREC_BF16, true, FAMILY_LOGISTIC, true>(a, n_chunks, s)
-                      : launch_c<NT, W, PREC_BF16, false, FAMILY_LOGISTIC, true>(a, n_chunks, s);
+        const int cm = (a.colmax ? 1 : 0) | (a.zcolmax ? 2 : 0);
+        if (cm == 1)
+          return std_ ? launch_c<NT, W, PREC_BF16, true, FAMILY_LOGISTIC, 1>(a, n_chunks, s)
+                      : launch_c<NT, W, PREC_BF16, false, FAMILY_LOGISTIC, 1>(a, n_chunks, s);
+        if (cm == 2)
+          return std_ ? launch_c<NT, W, PREC_BF16, true, FAMILY_LOGISTIC, 2>(a, n_chunks, s)
+                      : launch_c<NT, W, PREC_BF16, false, FAMILY_LOGISTIC, 2>(a, n_chunks, s);
+        if (cm == 3)
+          return std_ ? launch_c<NT, W, PREC_BF16, true, FAMILY_LOGISTIC, 3>(a, n_chunks, s)
+                      : launch_c<NT, W, PREC_BF16, false, FAMILY_LOGISTIC, 3>(a, n_chunks, s);
       }
       return std_ ? launch_c<NT, W, PREC_BF16, true, FAMILY_LOGISTIC>(a, n_chunks, s)
                   : launch_c<NT, W, PREC_BF16, false, FAMILY_LOGISTIC>(a, n_chunks, s);

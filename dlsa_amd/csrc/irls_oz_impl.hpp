@@ -105,6 +105,12 @@ constexpr int kMaxPiecesPerWave = 7;  // 1-KiB DMA pieces of a block per consume
 #ifndef DLSA_OZ_TICK
 #define DLSA_OZ_TICK 1
 #endif
+// DMA schedule of the consumers (profiling variants): 0 the next blocks'
+// pieces ticked through both images' MFMAs; 1 / 2 all of them during the
+// first image's (see the consumer loop)
+#ifndef DLSA_OZ_SCHED
+#define DLSA_OZ_SCHED 0
+#endif
 // consumers at s_setprio DLSA_OZ_PRIO: the younger half of the workgroup
 // otherwise gets only the producers' leftover issue slots (MI355X_MICROARCH.md
 // "Two waves per SIMD", items 2 and 4)
@@ -254,6 +260,8 @@ static inline int oz_prof_read_impl(unsigned long long* out) {
   return hipMemcpyToSymbol(HIP_SYMBOL(g_oz_prof), z, 16 * 8) == hipSuccess ? 0 : -1;
 }
 #define OZ_STAMP(v) const uint64_t v = __builtin_readcyclecounter()
+#define OZ_STAMP_VAR(v) uint64_t v = 0
+#define OZ_STAMP_SET(v) v = __builtin_readcyclecounter()
 #define OZ_ADD(i, d) prof[i] += (d)
 #define OZ_DECL uint64_t prof[6] = {0, 0, 0, 0, 0, 0}
 #define OZ_FLUSH(base)                                                        \
@@ -261,6 +269,8 @@ static inline int oz_prof_read_impl(unsigned long long* out) {
     for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&g_oz_prof[(base) + i_], prof[i_])
 #else
 #define OZ_STAMP(v)
+#define OZ_STAMP_VAR(v)
+#define OZ_STAMP_SET(v)
 #define OZ_ADD(i, d)
 #define OZ_DECL
 #define OZ_FLUSH(base)
@@ -528,22 +538,49 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
           if (DLSA_OZ_TICK && d1) issue_x(tI, l1, s1);
         };
         constexpr int I0 = DLSA_OZ_TICK ? TW : 0;
-        const bool c1 = m >= 1 && 2 * m - 1 < nb && !(DLSA_OZ_ABLATE & 2);
-        if (m >= 1 && !(DLSA_OZ_ABLATE & 2)) C.consume(slot_x(2 * m - 2), p, lane, tick0);
-        if (c1) C.consume(slot_x(2 * m - 1), p, lane, tick1);
-        OZ_STAMP(t2);
-        // pieces not yet issued: all of a block whose image tick did not run
-        if (d0) {
-          if (m >= 1 && !(DLSA_OZ_ABLATE & 2))
-            issue_rest(std::integral_constant<int, I0>{}, 2 * m + 2, l0, s0);
-          else
-            issue_rest(std::integral_constant<int, 0>{}, 2 * m + 2, l0, s0);
-        }
-        if (d1) {
-          if (c1)
-            issue_rest(std::integral_constant<int, I0>{}, 2 * m + 3, l1, s1);
-          else
-            issue_rest(std::integral_constant<int, 0>{}, 2 * m + 3, l1, s1);
+        const bool c0 = m >= 1 && !(DLSA_OZ_ABLATE & 2);
+        const bool c1 = c0 && 2 * m - 1 < nb;
+        OZ_STAMP_VAR(t2);
+        if constexpr (DLSA_OZ_SCHED == 0) {
+          if (c0) C.consume(slot_x(2 * m - 2), p, lane, tick0);
+          if (c1) C.consume(slot_x(2 * m - 1), p, lane, tick1);
+          OZ_STAMP_SET(t2);
+          // pieces not yet issued: all of a block whose image tick did not run
+          if (d0) {
+            if (c0)
+              issue_rest(std::integral_constant<int, I0>{}, 2 * m + 2, l0, s0);
+            else
+              issue_rest(std::integral_constant<int, 0>{}, 2 * m + 2, l0, s0);
+          }
+          if (d1) {
+            if (c1)
+              issue_rest(std::integral_constant<int, I0>{}, 2 * m + 3, l1, s1);
+            else
+              issue_rest(std::integral_constant<int, 0>{}, 2 * m + 3, l1, s1);
+          }
+        } else {
+          // both blocks' DMA during the first image's MFMAs (SCHED 1: a piece
+          // of each per tile; SCHED 2: block 2m+2 at once, then a piece of
+          // 2m+3 per tile), so the last pieces land while the second image's
+          // MFMAs run instead of in front of the iteration's final wait
+          auto tickA = [&](auto tI) {
+            if (DLSA_OZ_SCHED == 1 && d0) issue_x(tI, l0, s0);
+            if (d1) issue_x(tI, l1, s1);
+          };
+          auto tickN = [&](auto) {};
+          if (DLSA_OZ_SCHED == 2 && d0) issue_rest(std::integral_constant<int, 0>{}, 2 * m + 2, l0, s0);
+          if (c0) C.consume(slot_x(2 * m - 2), p, lane, tickA);
+          if (c0) {
+            if (DLSA_OZ_SCHED == 1 && d0)
+              issue_rest(std::integral_constant<int, TW>{}, 2 * m + 2, l0, s0);
+            if (d1) issue_rest(std::integral_constant<int, TW>{}, 2 * m + 3, l1, s1);
+          } else {
+            if (DLSA_OZ_SCHED == 1 && d0)
+              issue_rest(std::integral_constant<int, 0>{}, 2 * m + 2, l0, s0);
+            if (d1) issue_rest(std::integral_constant<int, 0>{}, 2 * m + 3, l1, s1);
+          }
+          if (c1) C.consume(slot_x(2 * m - 1), p, lane, tickN);
+          OZ_STAMP_SET(t2);
         }
         OZ_STAMP(t3);
         wv_wait_vmcnt<0>();
@@ -607,27 +644,46 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
       left[X] = nrows - b * RB;
     }
     // ---- row phase of both blocks: 8 rows per wave, 8 lanes per row ---------
+    // Two full blocks (every block but a chunk's last) read x unmasked: a
+    // feature f >= P of a row reads the row's successor in the same block (or,
+    // for the block's last row, the slot's y bytes): finite values of this
+    // chunk that meet beta_f = 0 in eta, and whose gradient and H entries the
+    // solve never reads (f >= P).  A chunk's last block(s) zero the rows past
+    // the chunk (they hold the next partition's rows, which must not leak
+    // into this one, not even as NaN) and the padding features.
+    const bool full = left[0] >= RB && left[1] >= RB;  // workgroup-uniform
     double xv[2][M], e[2], r[2];
+    auto row_phase = [&](auto maskI) {
+      constexpr bool MASK = decltype(maskI)::value;
 #pragma unroll
-    for (int X = 0; X < 2; ++X) {
-      const bool valid = rB < left[X];
-      const double* xr = (const double*)xsb[X] + rB * p + (sl - ic);
-      double e0 = 0.0, e1 = 0.0;
+      for (int X = 0; X < 2; ++X) {
+        const bool valid = rB < left[X];
+        const double* xr = (const double*)xsb[X] + rB * p + (sl - ic);
+        double e0 = 0.0, e1 = 0.0;
 #pragma unroll
-      for (int m2 = 0; m2 < M; ++m2) {
-        const int f = sl + LPR * m2;
-        double v = xr[LPR * m2];
-        if constexpr (STD) v = (v - stdv[f]) * stdv[PMAX + f];
-        if (m2 == 0 && ic && sl == 0) v = 1.0;
-        v = (valid && ((fmask >> m2) & 1u)) ? v : 0.0;
-        xv[X][m2] = v;
-        if (m2 & 1)
-          e1 = fma(v, beta[m2], e1);
-        else
-          e0 = fma(v, beta[m2], e0);
+        for (int m2 = 0; m2 < M; ++m2) {
+          const int f = sl + LPR * m2;
+          double v = xr[LPR * m2];
+          if constexpr (STD) v = (v - stdv[f]) * stdv[PMAX + f];
+          if (m2 == 0 && ic && sl == 0) v = 1.0;
+          if constexpr (MASK) {
+            // features below the smallest P of this NT are always < P
+            const bool fin = LPR * m2 + LPR - 1 < 16 * (NT - 1) + 1 || ((fmask >> m2) & 1u);
+            v = (valid && fin) ? v : 0.0;
+          }
+          xv[X][m2] = v;
+          if (m2 & 1)
+            e1 = fma(v, beta[m2], e1);
+          else
+            e0 = fma(v, beta[m2], e0);
+        }
+        e[X] = e0 + e1;
       }
-      e[X] = e0 + e1;
-    }
+    };
+    if (full)
+      row_phase(std::false_type{});
+    else
+      row_phase(std::true_type{});
 #pragma unroll
     for (int X = 0; X < 2; ++X) e[X] = wv_row_sum<RPW>(e[X]);
     // One transcendental chain for the 16 rows of both blocks: lanes 0-31 take

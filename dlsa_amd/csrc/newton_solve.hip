@@ -452,6 +452,8 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
         ph = PHASE_F64;
       } else {
         ph = approx_next_phase(a, k, ph, dm, ll, llp);
+        // near the switch: the next bf16 pass records the Ozaki digit scales
+        if (ph == PHASE_F32 && dm <= kOzNearTol * (1.0 + tm)) atomicAdd(&a.counters[3], 1);
       }
     } else if (dm <= a.tol * (1.0 + tm)) {
       a.status[k] = DLSA_STATUS_OK;

@@ -218,9 +218,9 @@ ELEM = 1e-10
 
 
 @pytest.mark.parametrize("kind", ["lognormal", "outlier", "separable"])
-@pytest.mark.parametrize("p_extra", [0, 93])
+@pytest.mark.parametrize("p_extra", [6, 93])
 def test_ozaki_heavy_tails_per_entry(torch_cuda, M, monkeypatch, kind, p_extra):
-    """Default mode, fused int8 exact pass (P = 8 and P = 101, NT 1 and 7):
+    """Default mode, fused int8 exact pass (P = 13-14 and 100-101, NT 1 and 7):
     the designs of heavy_design against the fp64 exact pass at the same
     iterate and against the oracle, entry by entry: max |dH_ij| / sqrt(H_ii
     H_jj) < 1e-10, theta within 1e-8.  (Digit exponents from the chunk's max

@@ -22,6 +22,10 @@ for v in "$@"; do
     wslot3) D=DLSA_WAVE_NSLOT=3 ;;
     word) D=DLSA_WAVE_ORDER=1 ;;
     ozprof) D=DLSA_OZ_PROF=1 ;;
+    ozs1) D=DLSA_OZ_SCHED=1 ;;
+    ozs2) D=DLSA_OZ_SCHED=2 ;;
+    ozs1prof) D="DLSA_OZ_SCHED=1 -DDLSA_OZ_PROF=1" ;;
+    ozs2prof) D="DLSA_OZ_SCHED=2 -DDLSA_OZ_PROF=1" ;;
     oz6) D=DLSA_OZ_LEVELS=6 ;;
     oztick0) D=DLSA_OZ_TICK=0 ;;
     ozprio0) D=DLSA_OZ_PRIO=0 ;;
@@ -32,5 +36,7 @@ for v in "$@"; do
     sc1) D=DLSA_X_DMA_AUX=1 ;;
     *) echo "unknown variant $v"; exit 1 ;;
   esac
-  python -c "from dlsa_amd.build import build; print(build(force=True, out='tools/_variants/libdlsa_hip_$v.so', defines='$D'.replace('-D', '').split()))"
+  ONLY=None
+  case $v in oz*|ozs*) ONLY='["irls_oz.hip", "irls_oz_g2.hip"]' ;; esac
+  python -c "from dlsa_amd.build import build; print(build(force=True, out='tools/_variants/libdlsa_hip_$v.so', defines='$D'.replace('-D', '').split(), only=$ONLY))"
 done
