@@ -77,17 +77,27 @@ constexpr int RB = 32;           // rows per DMA block
 constexpr int RPW = RB / NPW;    // rows per producer wave per block (8)
 constexpr int LPR = 64 / RPW;    // row-phase lanes per row (8)
 constexpr int NSLOT = 6;         // ring: 2 in flight, 2 producing, 2 consuming
-constexpr int ND = 5;            // digits
+// digits per value (DLSA_OZ_DIGITS: 5, the product; 4: a 30-bit grid, levels
+// 0-4 -- 8 MFMAs per tile and 32-row block instead of 9, one quad transpose
+// per value; ~5e-11 instead of ~2e-12 per entry in the numpy restatement; A/B
+// variant)
+#ifndef DLSA_OZ_DIGITS
+#define DLSA_OZ_DIGITS 5
+#endif
+constexpr int ND = DLSA_OZ_DIGITS;
+static_assert(ND == 4 || ND == 5, "4 or 5 digits");
+constexpr int GBITS = 8 * ND - 2;  // F = round(z 2^(GBITS - E)), |F| <= 2^GBITS
 // levels k = a + b of digit products kept (DLSA_OZ_LEVELS: 5, 6 or 7)
 #ifndef DLSA_OZ_LEVELS
 #define DLSA_OZ_LEVELS 5
 #endif
 constexpr int NL = DLSA_OZ_LEVELS;
-static_assert(NL >= 5 && NL <= 7, "5, 6 or 7 levels");
+static_assert((ND == 5 && NL >= 5 && NL <= 7) || (ND == 4 && NL == 5), "levels");
 constexpr int EMIN = -985;       // 2^(38 - EMIN) stays finite
 constexpr int EMAX = 1023;
-// 1.5 2^52 + 0x8080808080: t = fma(x, c, MAGIC) holds F + B in its low 40 bits
-constexpr double MAGIC = 6755399441055744.0 + 551911719040.0;
+// 1.5 2^52 + B, B = 0x8080808080 (0x80808080 for 4 digits): t = fma(x, c,
+// MAGIC) holds F + B in its low 8 ND bits
+constexpr double MAGIC = 6755399441055744.0 + (ND == 5 ? 551911719040.0 : 2155905152.0);
 
 // Ring slot: [16 B pad][x: the block's bytes from its 16-B-aligned start][y: 256 B].
 // The x span is cut to what the block needs (the last 1-KiB DMA piece runs
@@ -98,7 +108,7 @@ __host__ __device__ constexpr int slot_bytes(int p) { return 16 + xspan(p) + 256
 // a wave's image: [feature][digit plane][8 rows] bytes, 48 B per feature (5
 // planes + an unwritten sixth), so a lane's operand pair of planes (a, a+1),
 // a even, is one aligned 16-byte read
-constexpr int kFeatBytes = 48;
+constexpr int kFeatBytes = ND == 5 ? 48 : 32;
 constexpr int kMaxPiecesPerWave = 7;  // 1-KiB DMA pieces of a block per consumer wave
 // consumers issue the next blocks' DMA one piece per tile (1) or all before
 // their MFMAs (0)
@@ -317,7 +327,7 @@ struct OzConsumer {
         // A quad a: digits (a, a+1) of the feature -- one 16-byte read
         A0[u] = *(const oz_i4*)(im + fa);
         A2[u] = *(const oz_i4*)(im + fa + 16);
-        A4[u] = *(const u2*)(im + fa + 32);
+        if constexpr (ozk::ND == 5) A4[u] = *(const u2*)(im + fa + 32);
       };
       loadB(std::integral_constant<int, TL::J_of(0)>{}, 0);
       loadA(std::integral_constant<int, 0>{}, 0);
@@ -341,16 +351,32 @@ struct OzConsumer {
           Bq[b] = oz_i4{(int)d[b].x, (int)d[b].y, (int)d[b - 1].x, (int)d[b - 1].y};
         if constexpr (NB > 5) Bq[5] = oz_i4{0, 0, (int)d[4].x, (int)d[4].y};
         const oz_i4 a0 = A0[ua], a2 = A2[ua];
+        if constexpr (ozk::ND == 4) {  // levels 0-4: 8 MFMAs (level 4: (1,3) (2,2) (3,1))
+          const oz_i4 b4 = oz_i4{0, 0, (int)d[3].x, (int)d[3].y};
+          acc[t][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, Bq[0], acc[t][0], 0, 0, 0);
+          acc[t][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, Bq[1], acc[t][1], 0, 0, 0);
+          acc[t][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, Bq[2], acc[t][2], 0, 0, 0);
+          acc[t][3] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, Bq[3], acc[t][3], 0, 0, 0);
+          acc[t][4] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, b4, acc[t][4], 0, 0, 0);
+          acc[t][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a2, Bq[0], acc[t][2], 0, 0, 0);
+          acc[t][3] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a2, Bq[1], acc[t][3], 0, 0, 0);
+          acc[t][4] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a2, Bq[2], acc[t][4], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          tick(std::integral_constant<int, t>{});
+          return;
+        }
         const oz_i4 a4 = oz_i4{(int)A4[ua].x, (int)A4[ua].y, 0, 0};  // digit 5 = 0
         acc[t][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, Bq[0], acc[t][0], 0, 0, 0);
         acc[t][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, Bq[1], acc[t][1], 0, 0, 0);
         acc[t][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, Bq[2], acc[t][2], 0, 0, 0);
         acc[t][3] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, Bq[3], acc[t][3], 0, 0, 0);
-        acc[t][4] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, Bq[4], acc[t][4], 0, 0, 0);
-        acc[t][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a2, Bq[0], acc[t][2], 0, 0, 0);
-        acc[t][3] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a2, Bq[1], acc[t][3], 0, 0, 0);
-        acc[t][4] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a2, Bq[2], acc[t][4], 0, 0, 0);
-        acc[t][4] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a4, Bq[0], acc[t][4], 0, 0, 0);
+        if constexpr (ozk::ND == 5) {
+          acc[t][4] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, Bq[4], acc[t][4], 0, 0, 0);
+          acc[t][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a2, Bq[0], acc[t][2], 0, 0, 0);
+          acc[t][3] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a2, Bq[1], acc[t][3], 0, 0, 0);
+          acc[t][4] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a2, Bq[2], acc[t][4], 0, 0, 0);
+          acc[t][4] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a4, Bq[0], acc[t][4], 0, 0, 0);
+        }
         if constexpr (ozk::NL > 5) {  // level 5: (1,4) (2,3) (3,2) (4,1)
           acc[t][5] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, Bq[NB - 1], acc[t][5], 0, 0, 0);
           acc[t][5] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a2, Bq[3], acc[t][5], 0, 0, 0);
@@ -620,7 +646,7 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
   for (int m = 0; m < M; ++m) {
     const int f = sl + LPR * m;
     beta[m] = bet[f];
-    esc[m] = 38 - ex[f];
+    esc[m] = GBITS - ex[f];
     gacc[m] = 0.0;
     if (f < P) fmask |= 1u << m;
   }
@@ -742,9 +768,10 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
         gacc[m2] = fma(xv[X][m2], r[X], gacc[m2]);
         const double t = fma(xv[X][m2], __builtin_amdgcn_ldexp(sw[X], esc[m2]), MAGIC);
         const uint32_t lo = __double2loint(t);
-        // lane jq: byte jq of the quad's 4 rows = digit 4 - jq
+        // lane jq: byte jq of the quad's 4 rows = digit ND - 1 - jq
         const uint32_t dq = quad_transpose(lo, sel1, sel2) ^ 0x80808080u;
-        *(uint32_t*)(img + (sl + LPR * m2) * kFeatBytes + (4 - jq) * 8) = dq;
+        *(uint32_t*)(img + (sl + LPR * m2) * kFeatBytes + (ND - 1 - jq) * 8) = dq;
+        if constexpr (ND == 4) continue;  // the low dword held all four digits
         top[m2 & 3] = __double2hiint(t);
         if ((m2 & 3) == 3 || m2 == M - 1) {  // digit 0 of up to 4 features
           const int m0 = m2 & ~3, n = m2 - m0 + 1;

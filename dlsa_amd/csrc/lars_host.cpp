@@ -53,7 +53,7 @@ inline double dot(
   return (s0 + s1) + (s2 + s3);
 }
 
-// out[j] = Sp[j, 0..n) . w for every j in rows: four rows per pass share
+// out[j] = Sp[j, 0..n) . w for every j in rows (Sp: row-major, leading dimension ld): four rows per pass share
 // each load of w (AVX2 FMA, 2 accumulators per row)
 void dots_rows(int n, const double* Sp, size_t ld, const std::vector<int>& rows, const double* w,
                double* out) {
@@ -247,21 +247,24 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
     for (int j = 0; j < m; ++j) Sig[(size_t)i * m + j] *= absb[i] * absb[j];
   auto S = [&](int i, int j) { return Sig[(size_t)i * m + j]; };
 
-  // Sp: Sigma with its columns permuted so that the active set occupies the
-  // leading positions in `active` order (pos[j] = column position of
-  // variable j).  The equiangular correlations of an inactive column j are
-  // then one contiguous dot product Sp[j, 0..|A|) . w, and those of an active
-  // column are A * Sign exactly (Sigma_AA w = A Sigma_AA Sigma_AA^-1 Sign):
-  // (m - |A|) |A| multiply-adds per knot instead of m |A| strided row axpys
-  std::vector<double> Sp(Sig);
-  std::vector<int> perm(m), pos(m);
-  for (int j = 0; j < m; ++j) perm[j] = pos[j] = j;
-  auto swap_cols = [&](int p1, int p2) {
-    if (p1 == p2) return;
-    for (int i = 0; i < m; ++i) std::swap(Sp[(size_t)i * m + p1], Sp[(size_t)i * m + p2]);
-    std::swap(perm[p1], perm[p2]);
-    pos[perm[p1]] = p1;
-    pos[perm[p2]] = p2;
+  // SA: the active columns of Sigma, row-major (leading dimension m), column
+  // slot[q] holding active variable q.  The equiangular correlations of an
+  // inactive row j are then one contiguous dot product SA[j, 0..|A|) . w'
+  // (w' = w in slot order), and those of an active column are A * Sign
+  // exactly (Sigma_AA w = A Sigma_AA Sigma_AA^-1 Sign): (m - |A|) |A|
+  // multiply-adds per knot.  Adding a variable writes one column (its row of
+  // the symmetric Sigma); a lasso drop moves the last slot's column into the
+  // freed one -- no permutation of the whole matrix (the column swaps of
+  // round 2 touched two strided columns per added variable and re-sorted every
+  // active column after a drop).
+  std::vector<double> SA((size_t)m * m, 0.0);
+  std::vector<int> slot;
+  auto put_col = [&](int s_, int var) {
+    const double* src = &Sig[(size_t)var * m];
+    for (int i = 0; i < m; ++i) SA[(size_t)i * m + s_] = src[i];
+  };
+  auto move_col = [&](int from, int to) {
+    for (int i = 0; i < m; ++i) SA[(size_t)i * m + to] = SA[(size_t)i * m + from];
   };
 
   std::vector<double> Cvec(m, 0.0);
@@ -289,9 +292,10 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
   Chol R(m);
   int rank = 0;
   int k = 0;
-  std::vector<double> C, u, Gi1, w, a;
+  std::vector<double> C, u, Gi1, w, a, wslot;
   bool u_valid = false;
-  std::vector<int> inactive, keep;
+  std::vector<int> inactive;
+  std::vector<double> keepm;  // -1.0 (sign bit set) for the columns the step length scans
   while (k < max_steps && (int)active.size() < m) {
     ++k;
     inactive.clear();
@@ -333,7 +337,8 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
           ignores.push_back(j);
           in_ignores[j] = 1;
         } else {
-          swap_cols(pos[j], (int)active.size());
+          put_col((int)active.size(), j);
+          slot.push_back((int)active.size());
           active.push_back(j);
           in_active[j] = 1;
           Sign.push_back((Cvec[j] > 0) - (Cvec[j] < 0));
@@ -372,18 +377,41 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
     for (int q = 0; q < na; ++q) w[q] = A * Gi1[q];
     double gamhat = Cmax / A;
     // a = Sigma[:, active] w: the equiangular correlations of every column,
-    // used by the step length and by the correlation update (see Sp)
+    // used by the step length and by the correlation update (see SA)
     a.resize(m);
     inactive.clear();
     for (int j = 0; j < m; ++j)
       if (!in_active[j]) inactive.push_back(j);
-    dots_rows(na, Sp.data(), (size_t)m, inactive, w.data(), a.data());
+    wslot.assign(na, 0.0);
+    for (int q = 0; q < na; ++q) wslot[slot[q]] = w[q];
+    dots_rows(na, SA.data(), (size_t)m, inactive, wslot.data(), a.data());
     for (int q = 0; q < na; ++q) a[active[q]] = A * Sign[q];
     if (na < m) {
-      keep.clear();
-      for (int j = 0; j < m; ++j)
-        if (!in_active[j] && !in_ignores[j]) keep.push_back(j);
-      for (int j : keep) {
+      // min over the columns neither active nor ignored of the positive step
+      // lengths (Cmax -+ c_j) / (A -+ a_j): four columns per AVX2 pass (the same
+      // IEEE divisions and an exact min, so the result is that of the scalar
+      // loop)
+      keepm.resize(m);
+      for (int j = 0; j < m; ++j) keepm[j] = (!in_active[j] && !in_ignores[j]) ? -1.0 : 0.0;
+      const __m256d vC = _mm256_set1_pd(Cmax), vA = _mm256_set1_pd(A);
+      const __m256d veps = _mm256_set1_pd(eps), vinf = _mm256_set1_pd(INFINITY);
+      __m256d vg = _mm256_set1_pd(gamhat);
+      int j = 0;
+      for (; j + 4 <= m; j += 4) {
+        const __m256d aj = _mm256_loadu_pd(&a[j]), c = _mm256_loadu_pd(&Cvec[j]);
+        const __m256d keepv = _mm256_loadu_pd(&keepm[j]);  // all-ones sign bit where kept
+        const __m256d g1 = _mm256_div_pd(_mm256_sub_pd(vC, c), _mm256_sub_pd(vA, aj));
+        const __m256d g2 = _mm256_div_pd(_mm256_add_pd(vC, c), _mm256_add_pd(vA, aj));
+        const __m256d m1 = _mm256_and_pd(_mm256_cmp_pd(g1, veps, _CMP_GT_OQ), keepv);
+        const __m256d m2 = _mm256_and_pd(_mm256_cmp_pd(g2, veps, _CMP_GT_OQ), keepv);
+        vg = _mm256_min_pd(vg, _mm256_blendv_pd(vinf, g1, m1));
+        vg = _mm256_min_pd(vg, _mm256_blendv_pd(vinf, g2, m2));
+      }
+      double gv[4];
+      _mm256_storeu_pd(gv, vg);
+      gamhat = std::min(std::min(gv[0], gv[1]), std::min(gv[2], gv[3]));
+      for (; j < m; ++j) {
+        if (keepm[j] == 0.0) continue;
         const double aj = a[j];
         const double c = Cvec[j];
         const double g1 = (Cmax - c) / (A - aj), g2 = (Cmax + c) / (A + aj);
@@ -448,7 +476,23 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
       rank = R.d;
       R.rebuild_lt();
       u_valid = false;
-      std::vector<int> na_active;
+      // free the dropped slots: the column of the highest used slot moves in
+      int used = na;
+      for (int q = 0; q < na; ++q) {
+        if (!drops[q]) continue;
+        const int s_ = slot[q], last = used - 1;
+        if (s_ != last) {
+          for (int q2 = 0; q2 < na; ++q2)
+            if (slot[q2] == last) {
+              move_col(last, s_);
+              slot[q2] = s_;
+              break;
+            }
+        }
+        slot[q] = -1;
+        --used;
+      }
+      std::vector<int> na_active, na_slot;
       std::vector<double> na_sign;
       for (int q = 0; q < na; ++q) {
         if (drops[q]) {
@@ -456,12 +500,13 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
           in_active[active[q]] = 0;
         } else {
           na_active.push_back(active[q]);
+          na_slot.push_back(slot[q]);
           na_sign.push_back(Sign[q]);
         }
       }
       active.swap(na_active);
+      slot.swap(na_slot);
       Sign.swap(na_sign);
-      for (int q = 0; q < (int)active.size(); ++q) swap_cols(pos[active[q]], q);
     }
   }
 

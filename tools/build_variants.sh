@@ -23,6 +23,9 @@ for v in "$@"; do
     word) D=DLSA_WAVE_ORDER=1 ;;
     ozprof) D=DLSA_OZ_PROF=1 ;;
     ozs1) D=DLSA_OZ_SCHED=1 ;;
+    oz4d) D=DLSA_OZ_DIGITS=4 ;;
+    oz4dprof) D="DLSA_OZ_DIGITS=4 -DDLSA_OZ_PROF=1" ;;
+    oz4ds1) D="DLSA_OZ_DIGITS=4 -DDLSA_OZ_SCHED=1" ;;
     ozs2) D=DLSA_OZ_SCHED=2 ;;
     ozs1prof) D="DLSA_OZ_SCHED=1 -DDLSA_OZ_PROF=1" ;;
     ozs2prof) D="DLSA_OZ_SCHED=2 -DDLSA_OZ_PROF=1" ;;

@@ -5,7 +5,9 @@ set -o pipefail
 mkdir -p gpurun_out/r04f
 timeout -k 10 300 python -u -m pytest tests/test_gpu_ozaki.py -v --timeout 240 --timeout-method thread -k heavy \
     > gpurun_out/r04f/pytest_heavy.log 2>&1; tail -3 gpurun_out/r04f/pytest_heavy.log
-bash tools/gpu_oz_sched.sh r04f_sched || exit $?
+bash tools/gpu_oz_sched.sh r04f_sched base,ozs1,ozs2,oz4d,oz4ds1,ozprof,ozs1prof,oz4dprof || exit $?
+DLSA_LIB=tools/_variants/libdlsa_hip_oz4d.so timeout -k 10 300 python -u -m pytest tests/test_gpu_ozaki.py tests/test_gpu_parity.py -v --timeout 240 --timeout-method thread -k "ozaki or exact_pass or config1 or p100" \
+    > gpurun_out/r04f/pytest_oz4d.log 2>&1; tail -3 gpurun_out/r04f/pytest_oz4d.log
 bash tools/gpu_env_ab.sh r04f_zrec DLSA_OZ_ZREC=0 2 2 || exit $?
 bash tools/pmc.sh r04f_c4pmc --config 4 || exit $?
 CONFIGS=3 bash tools/pmc_configs.sh r04f_pmc || exit $?
