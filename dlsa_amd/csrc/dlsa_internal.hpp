@@ -30,13 +30,18 @@ enum : int32_t { STATUS_RUNNING = -1 };
 enum : int32_t { FAMILY_LOGISTIC = 0, FAMILY_GAUSSIAN = 1 };
 
 // Cache policy of the LDS-DMA loads that stream X (the aux / cpol operand of
-// buffer_load ... lds): X is read once per pass and is far larger than every
-// cache, so it streams non-temporally (2 = nt): config 2 76.3-76.9 vs
-// 77.6-77.9 ms per fit against the default policy in one A/B run
-// (profiles/r04a_nt_ab.txt); profiling builds override it
-// (tools/build_variants.sh).
+// buffer_load ... lds; profiling builds override it, tools/build_variants.sh).
+// The cooperative and per-wave passes keep the default policy: with nt (2)
+// the lines their consecutive blocks share are fetched twice (PMC, run r04g:
+// 842.6 vs 812.4 B/row for the config-2 bf16 pass, 624 vs 523 B/row for the
+// config-4 OLS pass, whose blocks are 8 rows); the Ozaki exact pass streams
+// non-temporally (813.6 vs 812.4 B/row, 17.6-18.0 vs 17.9-18.1 ms at config
+// 2 in two A/B runs, profiles/r04g_dma_policy_ab.txt).
 #ifndef DLSA_X_DMA_AUX
-#define DLSA_X_DMA_AUX 2
+#define DLSA_X_DMA_AUX 0
+#endif
+#ifndef DLSA_OZ_DMA_AUX
+#define DLSA_OZ_DMA_AUX 2
 #endif
 // Cooperative pass: 4 (8) waves per workgroup, 32-row blocks.
 constexpr int kCoopRows = 32;

@@ -523,7 +523,7 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
         if (j != np - 1 || lane * 16 < last_rem)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (wlds_void_t*)(smem + lds + 16 + j * 1024),
                                                    16, lane * 16, soff + j * 1024, 0,
-                                                   DLSA_X_DMA_AUX);
+                                                   DLSA_OZ_DMA_AUX);
       }
     };
     auto issue_y = [&](int blk, int lds) {

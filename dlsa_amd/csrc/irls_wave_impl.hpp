@@ -366,6 +366,11 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
   // OLS (w in {0, 1}): A operands are x itself (padded rows zeroed in the ring,
   // the intercept column = w)
   constexpr bool OLS_NOMUL = DLSA_WAVE_OLS_NOMUL && FAM == FAMILY_GAUSSIAN;
+  // OLS is one pass at theta = 0 (fit_impl: fit_init zeroes theta, max_iter =
+  // 1, no warm-start levels, no polish): eta = 0 and r = y, so the row phase
+  // skips the x . theta dot products and their row reductions -- fp64 VALU
+  // work that never co-executes with the fp64 MFMAs of the tile phase
+  constexpr bool ETA0 = FAM == FAMILY_GAUSSIAN;
 
   const int lane = threadIdx.x & 63;
   const int p = a.p, P = a.P, ic = a.intercept;
@@ -449,13 +454,15 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
         }
         if (m == 0 && ic && sl == 0) v = 1.0;
         xv[m] = v;
-        const double bm = bet[sl + LPR * m];
-        if (m & 1)
-          e1 = fma(v, bm, e1);
-        else
-          e0 = fma(v, bm, e0);
+        if constexpr (!ETA0) {
+          const double bm = bet[sl + LPR * m];
+          if (m & 1)
+            e1 = fma(v, bm, e1);
+          else
+            e0 = fma(v, bm, e0);
+        }
       }
-      const double e = wv_row_sum<RW>(e0 + e1);
+      const double e = ETA0 ? 0.0 : wv_row_sum<RW>(e0 + e1);
       const double yv = ys[row];
       double w, r;
       if constexpr (FAM == FAMILY_LOGISTIC) {

@@ -36,6 +36,7 @@ for v in "$@"; do
     ozab2) D="DLSA_OZ_ABLATE=2 -DDLSA_OZ_PROF=1" ;;
     ozab3) D="DLSA_OZ_ABLATE=3 -DDLSA_OZ_PROF=1" ;;
     nt) D=DLSA_X_DMA_AUX=2 ;;
+    dma0) D=DLSA_X_DMA_AUX=0 ;;
     sc1) D=DLSA_X_DMA_AUX=1 ;;
     *) echo "unknown variant $v"; exit 1 ;;
   esac
