@@ -10,7 +10,7 @@ hipError_t launch_irls_wave_g2(const PassArgs& a, int NT, bool std_, int family,
 
 // (the logistic ring is the larger one)
 int wave_lds_bytes(int NT, int p) {
-  return wave_lds_bytes_impl(NT, wave_rb(NT, wave_w(NT), FAMILY_LOGISTIC), p);
+  return wave_lds_bytes_impl(NT, wave_rb(NT, wave_w(NT), FAMILY_LOGISTIC), p, FAMILY_LOGISTIC);
 }
 
 hipError_t launch_irls_wave(const PassArgs& a, int NT, bool standardize, int family, int n_chunks,

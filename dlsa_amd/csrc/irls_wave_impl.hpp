@@ -153,12 +153,26 @@ __device__ __forceinline__ double wv_log12(double t) {
 
 }  // namespace
 
-// Ring slots per workgroup (DLSA_WAVE_NSLOT): 2 = one block in flight while
-// the current one is computed; 3 = two blocks in flight.
+// Ring slots per workgroup (DLSA_WAVE_NSLOT, DLSA_WAVE_NSLOT_OLS): 2 = one
+// block in flight while the current one is computed; 3 = two blocks in
+// flight.  Three slots for the OLS pass (8-row, 4 KiB blocks at P = 64) measured
+// slower (config-4 pass 16.7-17.1 vs 14.9-15.2 ms, profiles/r04h_ols_ab.txt).
 #ifndef DLSA_WAVE_NSLOT
 #define DLSA_WAVE_NSLOT 2
 #endif
-constexpr int kWaveSlots = DLSA_WAVE_NSLOT;
+#ifndef DLSA_WAVE_NSLOT_OLS
+#define DLSA_WAVE_NSLOT_OLS 2
+#endif
+__host__ __device__ constexpr int wave_slots(int FAM) {
+  return FAM == FAMILY_GAUSSIAN ? DLSA_WAVE_NSLOT_OLS : DLSA_WAVE_NSLOT;
+}
+// OLS without standardisation: a full block's row phase writes nothing the
+// other wave reads (w = 1 is a constant of the tile phase), so the barrier
+// between the row and tile phases can be kept for the tail block only
+// (DLSA_WAVE_OLS_ONESYNC = 1; not faster: 15.2 vs 14.9-15.0 ms, r04h)
+#ifndef DLSA_WAVE_OLS_ONESYNC
+#define DLSA_WAVE_OLS_ONESYNC 0
+#endif
 // Ring slot: [16 B pad][npieces KiB of X rows][256 B: y of up to 32 rows]
 __host__ __device__ __forceinline__ int wave_npieces(int RB, int p) {
   return (RB * p * 8 + 16 + 1023) / 1024;
@@ -168,8 +182,8 @@ __host__ __device__ __forceinline__ int wave_slot_bytes_impl(int RB, int p) {
 }
 // LDS of one workgroup: 2 ring slots + w of a block [RB] + theta [PMAX] +
 // center / 1/scale [2][PMAX]
-__host__ __device__ __forceinline__ int wave_lds_bytes_impl(int NT, int RB, int p) {
-  return kWaveSlots * wave_slot_bytes_impl(RB, p) + RB * 8 + 3 * 16 * NT * 8;
+__host__ __device__ __forceinline__ int wave_lds_bytes_impl(int NT, int RB, int p, int FAM) {
+  return wave_slots(FAM) * wave_slot_bytes_impl(RB, p) + RB * 8 + 3 * 16 * NT * 8;
 }
 
 // Waves per workgroup.  W = 2 (P <= 112): the T tiles are split over two
@@ -371,6 +385,8 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
   // skips the x . theta dot products and their row reductions -- fp64 VALU
   // work that never co-executes with the fp64 MFMAs of the tile phase
   constexpr bool ETA0 = FAM == FAMILY_GAUSSIAN;
+  constexpr int kWaveSlots = wave_slots(FAM);
+  constexpr bool ONESYNC = DLSA_WAVE_OLS_ONESYNC && OLS_NOMUL && !STD;
 
   const int lane = threadIdx.x & 63;
   const int p = a.p, P = a.P, ic = a.intercept;
@@ -485,7 +501,11 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
       for (int m = 0; m < M; ++m) gacc[m] = fma(xv[m], r, gacc[m]);
       if (sl == 0) wv[row] = w;
     }
-    if constexpr (W > 1) wv_sync<W>();  // w (and standardised x) of all rows visible
+    // w (and standardised / zeroed x) of all rows visible
+    if constexpr (W > 1) {
+      if (!ONESYNC || rows_left < RB) wv_sync<W>();  // workgroup-uniform
+    }
+    const bool w_one = ONESYNC && rows_left >= RB;  // full OLS block: w = 1 on every row
 
     // ---- tile phase: KS k-steps of 4 rows, this wave's TW tiles ---------------
     // operands of k-step s+1 are read while the MFMAs of k-step s run
@@ -500,7 +520,7 @@ __device__ __forceinline__ void wave_body(const PassArgs& a, const WaveCtx& cx, 
 #pragma unroll
         for (int r = 0; r < NS; ++r) xso[u][r] = xt[4 * r];
       }
-      wk[u] = wv[4 * s + q];
+      wk[u] = w_one ? 1.0 : wv[4 * s + q];
     };
     load(0, 0);
 #pragma unroll
@@ -617,6 +637,7 @@ __global__ __launch_bounds__(64 * W, wave_min_waves(NT, W, FAM)) void irls_wave_
   cx.nrows = __builtin_amdgcn_readfirstlane(a.chunk_rows[cx.chunk]);
   cx.nb = (cx.nrows + RB - 1) / RB;
   cx.npieces = wave_npieces(RB, p);
+  constexpr int kWaveSlots = wave_slots(FAM);
   cx.slot_bytes = wave_slot_bytes_impl(RB, p);
   cx.slot_y = 16 + cx.npieces * 1024;
   double* wv = (double*)(smem + kWaveSlots * cx.slot_bytes);
@@ -664,7 +685,7 @@ static inline int wave_w(int NT) {
 
 template <int NT, int W, bool STD, int FAM>
 static hipError_t launch_wave_t(const PassArgs& a, int n_chunks, hipStream_t s) {
-  const size_t lds = wave_lds_bytes_impl(NT, wave_rb(NT, W, FAM), a.p);
+  const size_t lds = wave_lds_bytes_impl(NT, wave_rb(NT, W, FAM), a.p, FAM);
   switch (wave_strip_ns(NT, a.P)) {
     case 1:
       hipLaunchKernelGGL((irls_wave_kernel<NT, 1, W, STD, FAM>), dim3(n_chunks), dim3(64 * W), lds,

@@ -20,6 +20,9 @@ for v in "$@"; do
     cat31) D=DLSA_CAT_ABLATE=31 ;;
     fab1) D=DLSA_FUSED_ABLATE=1 ;;
     wslot3) D=DLSA_WAVE_NSLOT=3 ;;
+    ols2slot) D=DLSA_WAVE_NSLOT_OLS=2 ;;
+    ols2sync) D=DLSA_WAVE_OLS_ONESYNC=0 ;;
+    olsr3) D="DLSA_WAVE_NSLOT_OLS=2 -DDLSA_WAVE_OLS_ONESYNC=0" ;;
     word) D=DLSA_WAVE_ORDER=1 ;;
     ozprof) D=DLSA_OZ_PROF=1 ;;
     ozs1) D=DLSA_OZ_SCHED=1 ;;
@@ -41,6 +44,9 @@ for v in "$@"; do
     *) echo "unknown variant $v"; exit 1 ;;
   esac
   ONLY=None
-  case $v in oz*|ozs*) ONLY='["irls_oz.hip", "irls_oz_g2.hip"]' ;; esac
+  case $v in
+    oz*|ozs*) ONLY='["irls_oz.hip", "irls_oz_g2.hip"]' ;;
+    ols*|wslot3) ONLY='["irls_wave.hip", "irls_wave_g2.hip"]' ;;
+  esac
   python -c "from dlsa_amd.build import build; print(build(force=True, out='tools/_variants/libdlsa_hip_$v.so', defines='$D'.replace('-D', '').split(), only=$ONLY))"
 done
