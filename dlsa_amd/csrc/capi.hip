@@ -1268,12 +1268,16 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
     const int64_t per = std::max<int64_t>(1, 512 / std::max(K, 1));
     return (int)std::max<int64_t>(1024, std::min<int64_t>((nmax + per - 1) / per, 1 << 24));
   };
-  // no warm-start levels: every categorical pass is exact and cheap, so the
-  // prefix levels' extra launches and host round trips cost more than the
-  // full-row passes they save (config 3: 11.2 ms per fit without levels,
-  // 14.9 ms with); DLSA_WARM_START=1 restores them (profiling knob)
+  // warm-start level (a 1/16 prefix of every partition, to a 0.2-relative
+  // step) only for partitions of >= 2^19 rows on average: every categorical
+  // pass is exact, so on small partitions the prefix passes' launches and host
+  // round trips cost more than the full pass they save (1.5e7 rows in 128
+  // partitions: 11.2 ms per fit without, 14.9 with, profiles r02), on large
+  // ones they save a full pass (config 3, 1.2e8 rows in 120 partitions: 37.2
+  // vs 38.7 ms per step, 7 vs 5 passes of which 4 vs 5 full,
+  // profiles/r04n_cat_warm_start_ab.txt).  DLSA_WARM_START overrides.
   std::vector<Plan> plans;
-  opt.warm_start = 0;
+  opt.warm_start = opt.warm_start && K > 0 && n_total / K >= (int64_t(1) << 19);
   if (const char* e = getenv("DLSA_WARM_START")) opt.warm_start = atoi(e);
   if (opt.warm_start) {
     const int64_t min_rows = std::max<int64_t>(2048, 64LL * P);

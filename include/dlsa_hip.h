@@ -235,8 +235,8 @@ int dlsa_logistic_loglik_batched(const double* X, const double* y,
  * all-zero outputs, the reference's "fake zero matrix".  Codes >= levels[f]
  * fail the call with DLSA_E_INVALID.  Limits: F <= 16, levels[f] in 1..256,
  * fit_intercept + q <= 16.  levels is a HOST array [F]; opt may be NULL
- * (hessian_mode and warm_start are ignored: every pass is exact fp64 and
- * runs on all rows).
+ * (hessian_mode is ignored: every pass is exact; warm_start runs a 1/16-prefix
+ * level first only when the partitions average >= 2^19 rows).
  */
 int dlsa_logistic_fit_categorical(const double* Xn, const uint8_t* codes, const double* y,
                                   const int64_t* offsets, int32_t K, int32_t q, int32_t F,
