@@ -510,6 +510,13 @@ def main():
     # describe the same launch
     pmc_file = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_file):
+        try:  # the int8 exact pass's own record (config 2), beside its kernel entry
+            ex = json.load(open(pmc_file)).get(f"config{args.config}_exact", {})
+            if not wide and not codes_layout and n_oz and ex.get("p") == p:
+                kern[exact]["traffic_bytes_per_row"] = ex["hbm_bytes_per_row"]
+                kern[exact]["traffic_source"] = ex.get("source")
+        except Exception:
+            pass
         try:
             rec = json.load(open(pmc_file)).get(f"config{args.config}", {})
             if rec.get("p") == p and rec.get("kernel_key") == pmc_key and \
