@@ -321,16 +321,18 @@ void irls_coop_kernel(const PassArgs a) {
 #pragma unroll
   for (int m = 0; m < M; ++m) asm volatile("" : "+v"(beta[m]));
   double llacc = 0.0;
-  // CM: running max of |x| per feature.  One v_max_f64 with the abs modifier
-  // per value and no row mask: the rows of a chunk's last block past its end
-  // are the next chunk's rows (or the range check's zeros), so the recorded
-  // max is an upper bound over the chunk's rows, which is all the digit
-  // exponents need (a looser bound only moves the digits down a bit).
-  double cmx[(CM & 1) ? M : 1];
+  // CM: running max of |x| per feature, kept as the high dword of |x| (what
+  // the digit exponents read: ozk::xbound sets the low dword to all ones) --
+  // 32-bit integer max instead of a v_max_f64 per value, half the registers.
+  // No row mask: the rows of a chunk's last block past its end are the next
+  // chunk's rows (or the range check's zeros), so the recorded max is an upper
+  // bound over the chunk's rows, which is all the digit exponents need (a
+  // looser bound only moves the digits down a bit).
+  uint32_t cmx[(CM & 1) ? M : 1];
   float zmx[(CM & 2) ? M : 1];  // running max |z| (fp32 image values; rows past the end have w = 0)
 #pragma unroll
   for (int m = 0; m < (CM ? M : 1); ++m) {
-    if constexpr (CM & 1) cmx[m] = 0.0;
+    if constexpr (CM & 1) cmx[m] = 0u;
     if constexpr (CM & 2) zmx[m] = 0.0f;
   }
   int tI[G::TPW], tJ[G::TPW];  // this wave's tiles (bf16 path)
@@ -411,7 +413,7 @@ void irls_coop_kernel(const PassArgs a) {
         if constexpr (STD) v = (v - stdv[sl + LPR * m]) * stdv[G::PMAX + sl + LPR * m];
         if (m == 0 && ic && sl == 0) v = 1.0;
         xv[m] = v;
-        if constexpr (CM & 1) asm("v_max_f64 %0, %0, |%1|" : "+v"(cmx[m]) : "v"(v));
+        if constexpr (CM & 1) cmx[m] = max(cmx[m], (uint32_t)__double2hiint(v) & 0x7FFFFFFFu);
         if (m & 1)
           e1 = fma(v, beta[m], e1);
         else
@@ -539,7 +541,7 @@ void irls_coop_kernel(const PassArgs a) {
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       uint32_t v = 0, u = 0;
-      if constexpr (CM & 1) v = __double2hiint(cmx[m]) & 0x7FFFFFFFu;
+      if constexpr (CM & 1) v = cmx[m];
       if constexpr (CM & 2) u = __float_as_uint(zmx[m]) & 0x7FFFFFFFu;  // ordered as integers
 #pragma unroll
       for (int o = 1; o < RPW; o <<= 1) {
