@@ -140,6 +140,10 @@ def test_config3_reference_partition_policy(torch_cuda, M):
     assert (np.diff(off) == 1_000_000).all()
     fit = M.logistic_model_batched_categorical(Xn, codes, y, off, levels, fit_intercept=True)
     assert (fit.status.cpu().numpy() == 0).all(), fit.status_counts()
+    # partitions of >= 2^19 rows run a 1/16-prefix warm-start level first
+    # (capi.hip fit_categorical): some passes streamed fewer than all n rows
+    st = fit.stats
+    assert st["rows_fp64"] < st["passes_fp64"] * n, st
     Xd = M.expand_categorical(Xn, codes, levels)
     Xd = torch.cat([torch.ones((n, 1), dtype=torch.float64, device=Xd.device), Xd], 1)
     a, b = int(off[1]), int(off[2])
