@@ -94,7 +94,8 @@ constexpr int GBITS = 8 * ND - 2;  // F = round(z 2^(GBITS - E)), |F| <= 2^GBITS
 constexpr int NL = DLSA_OZ_LEVELS;
 static_assert((ND == 5 && NL >= 5 && NL <= 7) || (ND == 4 && NL == 5), "levels");
 constexpr int EMIN = -985;       // 2^(38 - EMIN) stays finite
-constexpr int EMAX = 1023;
+constexpr int EMAX = 1009;       // MAGIC 2^(EMAX - 38) stays finite (|z| >= 2^1009
+                                 // overflows the fp64 Gram anyway)
 // 1.5 2^52 + B, B = 0x8080808080 (0x80808080 for 4 digits): t = fma(x, c,
 // MAGIC) holds F + B in its low 8 ND bits
 constexpr double MAGIC = 6755399441055744.0 + (ND == 5 ? 551911719040.0 : 2155905152.0);
@@ -115,17 +116,27 @@ constexpr int kMaxPiecesPerWave = 7;  // 1-KiB DMA pieces of a block per consume
 #ifndef DLSA_OZ_TICK
 #define DLSA_OZ_TICK 1
 #endif
-// DMA schedule of the consumers (profiling variants): 0 the next blocks'
-// pieces ticked through both images' MFMAs; 1 / 2 all of them during the
-// first image's (see the consumer loop)
+// DMA schedule of the consumers: 0 the next blocks' pieces ticked through
+// both images' MFMAs; 1 (the product since round 4) / 2 all of them during
+// the first image's (see the consumer loop)
 #ifndef DLSA_OZ_SCHED
-#define DLSA_OZ_SCHED 0
+#define DLSA_OZ_SCHED 1
 #endif
 // consumers at s_setprio DLSA_OZ_PRIO: the younger half of the workgroup
 // otherwise gets only the producers' leftover issue slots (MI355X_MICROARCH.md
 // "Two waves per SIMD", items 2 and 4)
 #ifndef DLSA_OZ_PRIO
 #define DLSA_OZ_PRIO 1
+#endif
+// producer digits (DLSA_OZ_DBATCH 1): the digit words of a block's values are
+// formed for all features first, then transposed stage by stage, so the
+// DPP / v_perm chains of different features interleave
+#ifndef DLSA_OZ_DBATCH
+#define DLSA_OZ_DBATCH 1
+#endif
+// per-feature magic constants instead of a per-value ldexp (DLSA_OZ_MAGICF 1)
+#ifndef DLSA_OZ_MAGICF
+#define DLSA_OZ_MAGICF 1
 #endif
 // profiling-only ablations (bits): 1 producers skip the row phase and digits, 2
 // consumers skip the MFMAs
@@ -284,6 +295,12 @@ static inline int oz_prof_read_impl(unsigned long long* out) {
 #define OZ_ADD(i, d)
 #define OZ_DECL
 #define OZ_FLUSH(base)
+#endif
+
+#if DLSA_OZ_MAGICF
+#define OZ_DIGIT_T(x, s, m) fma(x, s, mg[m])
+#else
+#define OZ_DIGIT_T(x, s, m) fma(x, __builtin_amdgcn_ldexp(s, esc[m]), MAGIC)
 #endif
 
 // ---- consumer waves: tiles of X^T W X -------------------------------------
@@ -640,13 +657,24 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
   const uint32_t sel2 = (lane & 2) ? 0x03020706u : 0x05040100u;
   const int jq = lane & 3;               // lane in its quad: digit plane 4 - jq
   double beta[M], gacc[M];
-  int esc[M];                            // 38 - E_f of this lane's features
+  // per-feature magic MAGIC 2^(E_f - 38): fma(x, sqrt(w), mg) carries the
+  // mantissa of fma(x, sqrt(w) 2^(38 - E_f), MAGIC) (a power-of-two scaling
+  // of the same rounding), so no per-value ldexp
+#if DLSA_OZ_MAGICF
+  double mg[M];
+#else
+  int esc[M];
+#endif
   uint32_t fmask = 0;                    // features f < P of this lane
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     const int f = sl + LPR * m;
     beta[m] = bet[f];
+#if DLSA_OZ_MAGICF
+    mg[m] = __builtin_amdgcn_ldexp(MAGIC, ex[f] - GBITS);
+#else
     esc[m] = GBITS - ex[f];
+#endif
     gacc[m] = 0.0;
     if (f < P) fmask |= 1u << m;
   }
@@ -758,6 +786,42 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
     OZ_STAMP(t2);
     OZ_ADD(1, t2 - t1);
     // ---- gradient and the digit images --------------------------------------
+#if DLSA_OZ_DBATCH
+    static_assert(ND == 5, "batched digits: 5 digits");
+    constexpr int NG = (M + 3) / 4;  // digit-0 words (4 features each)
+#pragma unroll
+    for (int X = 0; X < 2; ++X) {
+      char* img = xsb[X] + pw * RPW * p * 8 + k4 * 4;
+      uint32_t w[M + NG], hi[M];
+#pragma unroll
+      for (int m2 = 0; m2 < M; ++m2) {
+        gacc[m2] = fma(xv[X][m2], r[X], gacc[m2]);
+        const double t = OZ_DIGIT_T(xv[X][m2], sw[X], m2);
+        w[m2] = __double2loint(t);
+        hi[m2] = __double2hiint(t);
+      }
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        const int m0 = 4 * g, n = M - m0 < 4 ? M - m0 : 4;
+        const uint32_t h0 = hi[m0], h1 = n > 1 ? hi[m0 + 1] : h0;
+        const uint32_t h2 = n > 2 ? hi[m0 + 2] : h0, h3 = n > 3 ? hi[m0 + 3] : h0;
+        w[M + g] = perm(perm(h3, h2, 0x05010400u), perm(h1, h0, 0x05010400u), 0x05040100u);
+      }
+      // the quad transposes stage by stage over all words (independent chains)
+#pragma unroll
+      for (int i = 0; i < M + NG; ++i) w[i] = perm(dpp<0xB1>(w[i]), w[i], sel1);
+#pragma unroll
+      for (int i = 0; i < M + NG; ++i) w[i] = perm(dpp<0x4E>(w[i]), w[i], sel2) ^ 0x80808080u;
+#pragma unroll
+      for (int m2 = 0; m2 < M; ++m2)
+        *(uint32_t*)(img + (sl + LPR * m2) * kFeatBytes + (ND - 1 - jq) * 8) = w[m2];
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        const int m0 = 4 * g, n = M - m0 < 4 ? M - m0 : 4;
+        if (jq < n) *(uint32_t*)(img + (sl + LPR * (m0 + jq)) * kFeatBytes) = w[M + g];
+      }
+    }
+#else
 #pragma unroll
     for (int X = 0; X < 2; ++X) {
       // this wave's image over its own rows (read above): [feature][plane][8 rows]
@@ -766,7 +830,7 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
 #pragma unroll
       for (int m2 = 0; m2 < M; ++m2) {
         gacc[m2] = fma(xv[X][m2], r[X], gacc[m2]);
-        const double t = fma(xv[X][m2], __builtin_amdgcn_ldexp(sw[X], esc[m2]), MAGIC);
+        const double t = OZ_DIGIT_T(xv[X][m2], sw[X], m2);
         const uint32_t lo = __double2loint(t);
         // lane jq: byte jq of the quad's 4 rows = digit ND - 1 - jq
         const uint32_t dq = quad_transpose(lo, sel1, sel2) ^ 0x80808080u;
@@ -784,6 +848,7 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
         }
       }
     }
+#endif
 #ifdef DLSA_OZ_PROF
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #endif

@@ -26,11 +26,18 @@ for v in "$@"; do
     word) D=DLSA_WAVE_ORDER=1 ;;
     ozprof) D=DLSA_OZ_PROF=1 ;;
     ozs1) D=DLSA_OZ_SCHED=1 ;;
-    oz4d) D=DLSA_OZ_DIGITS=4 ;;
-    oz4dprof) D="DLSA_OZ_DIGITS=4 -DDLSA_OZ_PROF=1" ;;
-    oz4ds1) D="DLSA_OZ_DIGITS=4 -DDLSA_OZ_SCHED=1" ;;
+    oz4d) D="DLSA_OZ_DIGITS=4 -DDLSA_OZ_DBATCH=0" ;;
+    oz4dprof) D="DLSA_OZ_DIGITS=4 -DDLSA_OZ_DBATCH=0 -DDLSA_OZ_PROF=1" ;;
+    oz4ds1) D="DLSA_OZ_DIGITS=4 -DDLSA_OZ_DBATCH=0" ;;
     ozs2) D=DLSA_OZ_SCHED=2 ;;
     ozs1prof) D="DLSA_OZ_SCHED=1 -DDLSA_OZ_PROF=1" ;;
+    ozold) D="DLSA_OZ_MAGICF=0 -DDLSA_OZ_SCHED=0 -DDLSA_OZ_DBATCH=0" ;;
+    ozs0) D="DLSA_OZ_SCHED=0" ;;
+    ozdb0) D="DLSA_OZ_DBATCH=0" ;;
+    ozm0) D="DLSA_OZ_MAGICF=0" ;;
+    ozoldprof) D="DLSA_OZ_MAGICF=0 -DDLSA_OZ_PROF=1" ;;
+    ozdb) D="DLSA_OZ_DBATCH=1" ;;
+    ozs1db) D="DLSA_OZ_SCHED=1 -DDLSA_OZ_DBATCH=1" ;;
     ozs2prof) D="DLSA_OZ_SCHED=2 -DDLSA_OZ_PROF=1" ;;
     oz6) D=DLSA_OZ_LEVELS=6 ;;
     oztick0) D=DLSA_OZ_TICK=0 ;;

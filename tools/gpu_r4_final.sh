@@ -3,7 +3,7 @@
 # (rocprofv3 --kernel-trace --stats) of configs 2-5 and HBM-traffic PMC passes
 # (FETCH_SIZE, WRITE_SIZE; one counter group per run) of configs 2, 4 and 5.
 set -o pipefail
-OUT=gpurun_out/r04z; mkdir -p $OUT; export TMPDIR=/tmp
+OUT=gpurun_out/${TAG:-r04z}; mkdir -p $OUT; export TMPDIR=/tmp
 echo "[final] $(date +%T) pytest"
 timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
 rc=$?; tail -3 $OUT/pytest_gpu.log; grep -E "FAILED" $OUT/pytest_gpu.log | head -20
