@@ -107,6 +107,15 @@ def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()
         if res.returncode != 0:
             sys.stderr.write(res.stdout + res.stderr)
             raise RuntimeError(f"link failed ({res.returncode})")
+    # every symbol must resolve at load time: a kernel template whose host
+    # stub the compiler silently dropped links fine and only fails at dlopen
+    # (checked in a child process, so this one keeps no HIP library loaded)
+    chk = subprocess.run([sys.executable, "-c",
+                          "import ctypes, os, sys; ctypes.CDLL(sys.argv[1], mode=os.RTLD_NOW)",
+                          out + ".tmp"], capture_output=True, text=True)
+    if chk.returncode != 0:
+        sys.stderr.write(chk.stderr)
+        raise RuntimeError(f"{out}.tmp does not load (unresolved symbols)")
     os.replace(out + ".tmp", out)
     return out
 
