@@ -6,6 +6,10 @@ OUT=gpurun_out/${TAG:-ozops}; mkdir -p $OUT; export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread -k "ozaki or heavy or config2" > $OUT/pytest.log 2>&1; rc=$?
 tail -2 $OUT/pytest.log; grep -E "FAILED" $OUT/pytest.log | head
 [ $rc -eq 0 ] || exit $rc
+for v in $VARIANT_TEST; do  # the int8 tests on a variant build
+  DLSA_LIB=tools/_variants/libdlsa_hip_$v.so timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread -k "ozaki or config2" > $OUT/pytest_$v.log 2>&1; rc=$?
+  echo "$v: $(tail -1 $OUT/pytest_$v.log)"; [ $rc -eq 0 ] || exit $rc
+done
 timeout -k 10 600 python -u tools/pass_bench.py --n 25000000 --p 100 --K 256 --rounds 3 \
     --libs ${LIBS:-base,ozold,ozs1,ozbt,ozdb,ozprof,ozs1prof,ozoldprof} > $OUT/pass_bench.jsonl 2> $OUT/pass_bench.err
 rc=$?; cat $OUT/pass_bench.jsonl; tail -3 $OUT/pass_bench.err; [ $rc -eq 0 ] || exit $rc
