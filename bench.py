@@ -219,6 +219,8 @@ def main():
                     help="partitions of the CPU baseline sample (0: ~10-30 s of CPU work per config)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-fp64-step", action="store_true",
+                    help="skip the two untimed fp64-Sig_inv steps reported beside the line")
     ap.add_argument("--seed", type=int, default=2019)
     ap.add_argument("--layout", default="codes", choices=["codes", "dense"],
                     help="config 3: categorical-code layout (LDS-histogram pass) or the dense "
@@ -313,7 +315,7 @@ def main():
     stats_acc = []
     stage_ms = {"fit": 0.0, "reduce_allreduce": 0.0, "wlse_lars_dbic": 0.0}
 
-    def step(record):
+    def step(record, hessian=None, exact="auto"):
         nonlocal ws
         t_a = time.perf_counter()
         if family == "ols":
@@ -324,8 +326,9 @@ def main():
                                                      record_timing=record, device=dev)
         else:
             fit = logistic_model_batched(X, y, offsets, fit_intercept=fit_intercept,
-                                         hessian=args.hessian, tol=args.tol,
-                                         record_timing=record, workspace=ws, device=dev)
+                                         hessian=hessian or args.hessian, tol=args.tol,
+                                         record_timing=record, workspace=ws, device=dev,
+                                         exact=exact)
             if ws.numel() < fit.stats["workspace_bytes"]:
                 ws = torch.empty((fit.stats["workspace_bytes"],), dtype=torch.uint8, device=dev)
         t_b = time.perf_counter()  # the fit returns after its stream synchronisation
@@ -367,6 +370,19 @@ def main():
     assert K_red == K_job and n_red == n_job, (K_red, n_red, K_job, n_job)
     ms_per_step = elapsed / args.steps * 1e3
     value = n_job * args.steps / elapsed
+
+    # the same step with an fp64-MFMA Sig_inv, beside the headline line (one
+    # step each, after the timed region; N = 1 without a process group only,
+    # since a rank-0-only step would wait in the all-reduce)
+    fp64_steps = {}
+    if family == "logistic" and not codes_layout and not use_pg and not args.no_fp64_step:
+        for key, hs, ex in (("sig_inv_fp64_ms_per_step", "fp64", "fp64"),
+                            ("exact_fp64_ms_per_step", None, "fp64")):
+            torch.cuda.synchronize()
+            t_f = time.perf_counter()
+            step(False, hessian=hs, exact=ex)
+            torch.cuda.synchronize()
+            fp64_steps[key] = (time.perf_counter() - t_f) * 1e3
 
     # ---- per-kernel throughput and the roofline of the dominant kernel -----
     # (HIP events recorded on the fit's stream around every launch)
@@ -573,6 +589,11 @@ def main():
                    "n_chunks": last["n_chunks"],
                    "status": fit.status_counts()},
         "dbic_support_size": int(len(support)),
+        **fp64_steps,
+        **({"fp64_steps_note": (
+            "one untimed step each after the timed region: sig_inv_fp64 = --hessian fp64 (every "
+            "pass on the fp64 MFMA); exact_fp64 = the mixed schedule with the exact pass on the "
+            "fp64 MFMA (DLSA_EXACT_FP64) instead of the int8 digit slices")} if fp64_steps else {}),
         "algorithmic": {"bytes_per_pass": n * row_bytes, "flops_per_pass": n * alg_flops_row},
     }
     if rank == 0 and not args.no_parity:

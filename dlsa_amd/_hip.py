@@ -22,6 +22,8 @@ STATUS_NAMES = {0: "ok", 1: "maxiter", 2: "singular", 3: "empty", 4: "nonfinite"
 HESSIAN_MIXED = 0
 HESSIAN_FP64 = 1
 HESSIAN_MIXED_F32 = 2
+EXACT_AUTO = 0   # exact (Sig_inv) pass on the int8 cores where it applies
+EXACT_FP64 = 1   # exact pass on the fp64 MFMA
 MAX_P_FUSED = 192
 MAX_P = 512
 
@@ -39,7 +41,10 @@ class FitOptions(ctypes.Structure):
         ("workspace_bytes", ctypes.c_int64),
         ("rows_per_chunk", ctypes.c_int32),
         ("warm_start", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 6),
+        ("exact_pass", ctypes.c_int32),
+        ("exact_waves", ctypes.c_int32),
+        ("oz_max_bytes", ctypes.c_int64),
+        ("reserved", ctypes.c_int32 * 2),
     ]
 
 

@@ -74,7 +74,7 @@ struct Plan {
 // by the old rule) 3072 / 6144-row chunks fit 12.8 / 12.7 ms against 13.5 ms
 // (fewer per-chunk prologues and partial tiles; r02am).
 static int auto_rows_per_chunk(int64_t n_total) {
-  if (const char* e = getenv("DLSA_ROWS_PER_CHUNK")) return std::max(64, atoi(e));
+  if (const char* e = env_knob("DLSA_ROWS_PER_CHUNK")) return std::max(64, atoi(e));
   // rounded up to a multiple of 1024: equal partitions then split into whole
   // chunks (config 2: 16384 rows, 6 per partition) instead of a ragged extra one
   int64_t r = (n_total / 6144 + 1023) / 1024 * 1024;
@@ -101,7 +101,7 @@ static int64_t rows_used(int64_t nk, double frac, int64_t min_rows) {
 static std::vector<double> warm_level_fracs(bool fused) {
   std::vector<double> f = fused ? std::vector<double>{1.0 / 16.0}
                                 : std::vector<double>{1.0 / 16.0, 1.0 / 4.0};
-  if (const char* e = getenv("DLSA_LEVELS")) {
+  if (const char* e = env_knob("DLSA_LEVELS")) {
     f.clear();
     for (const char* s = e; *s;) {
       char* end = nullptr;
@@ -143,7 +143,7 @@ static int32_t* pinned_staging(size_t n_i32) {
 }
 
 static double warm_level_tol(bool fused) {
-  if (const char* e = getenv("DLSA_LEVEL_TOL")) return atof(e);
+  if (const char* e = env_knob("DLSA_LEVEL_TOL")) return atof(e);
   return fused ? 0.2 : 0.1;
 }
 
@@ -254,7 +254,7 @@ static void make_wide_plans(const int64_t* offsets, int K, int p, int intercept,
   int rpc_gram = (int)std::max<int64_t>(1024, std::min<int64_t>((n_total + groups - 1) / groups,
                                                                 int64_t(1) << 24));
   if (rows_per_chunk > 0) rpc_row = rpc_gram = rows_per_chunk;
-  if (const char* e = getenv("DLSA_WIDE_GRAM_ROWS")) rpc_gram = std::max(64, atoi(e));
+  if (const char* e = env_knob("DLSA_WIDE_GRAM_ROWS")) rpc_gram = std::max(64, atoi(e));
   // the Gram kernels address a row group's X with 32-bit buffer offsets
   rpc_gram = (int)std::min<int64_t>(rpc_gram, (int64_t(1) << 30) / (8LL * std::max(p, 1)));
   make_plan(offsets, K, p, intercept, rpc_row, wp.rows, frac, min_rows);
@@ -549,17 +549,14 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
   // digit records fit the workspace: the caller's (dlsa_logistic_workspace_bytes
   // counts them) or the one allocated here.  Without room for them -- a
   // caller workspace of at least base_total but less than total bytes, a
-  // failed allocation, or DLSA_WIDE_OZ_MAX_BYTES below the records' size --
-  // the fp64 Gram runs (stats.oz_fallbacks).  DLSA_OZ=0: always the fp64 Gram.
-  bool use_wide_oz = !(getenv("DLSA_OZ") && atoi(getenv("DLSA_OZ")) == 0) &&
-                     family == FAMILY_LOGISTIC && opt.hessian_mode == DLSA_HESSIAN_MIXED &&
-                     L.digit_bytes > 0;
-  if (use_wide_oz)
-    if (const char* e = getenv("DLSA_WIDE_OZ_MAX_BYTES"))
-      if (L.digit_bytes > atoll(e)) {
-        use_wide_oz = false;
-        g_stats.oz_fallbacks++;
-      }
+  // failed allocation, or opt.oz_max_bytes below the records' size -- the
+  // fp64 Gram runs (stats.oz_fallbacks).  DLSA_EXACT_FP64: always the fp64 Gram.
+  bool use_wide_oz = opt.exact_pass != DLSA_EXACT_FP64 && family == FAMILY_LOGISTIC &&
+                     opt.hessian_mode == DLSA_HESSIAN_MIXED && L.digit_bytes > 0;
+  if (use_wide_oz && opt.oz_max_bytes > 0 && L.digit_bytes > opt.oz_max_bytes) {
+    use_wide_oz = false;
+    g_stats.oz_fallbacks++;
+  }
   char* ws = (char*)opt.workspace;
   bool owned = false;
   if (!ws) {
@@ -962,6 +959,7 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
   pa.p = p;
   pa.P = P;
   pa.intercept = fit_intercept ? 1 : 0;
+  pa.waves = opt.exact_waves;
   const int approx_prec = opt.hessian_mode == DLSA_HESSIAN_MIXED_F32 ? PREC_F32 : PREC_BF16;
   // cooperative-pass LDS ring: two workgroups per CU (P <= 112) so that one's
   // row phase and barrier waits overlap the other's tile phase (measured
@@ -1012,15 +1010,14 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
 
   const bool trace = getenv("DLSA_TRACE") != nullptr;
   int32_t* h_phase = h_cnt + 4;  // [K] phases (pinned: no staging copy per iteration)
-  // exact passes on the int8 matrix cores (irls_oz_impl.hpp) unless DLSA_OZ=0:
+  // exact passes on the int8 matrix cores (irls_oz_impl.hpp) unless DLSA_EXACT_FP64:
   // the first full-data bf16 pass records, per chunk and feature, max |x|; the
   // bf16 passes that follow an iteration with a partition near the switch
   // (counters[3], kOzNearTol) record max |sqrt(w) x| at the theta they saw
   // (snapshotted into theta_rec first); the exact passes of the final plan
   // take their digit scales from the partition's last records (a chunk with
   // no max |z| record -- zcolmax = +inf, theta_rec = 0 -- gets max |x| / 2)
-  const bool use_oz = !(getenv("DLSA_OZ") && atoi(getenv("DLSA_OZ")) == 0) &&
-                      approx_prec == PREC_BF16 && oz_applies(pl.NT, p) &&
+  const bool use_oz = opt.exact_pass != DLSA_EXACT_FP64 && approx_prec == PREC_BF16 && oz_applies(pl.NT, p) &&
                       pl.max_chunk_rows <= kOzMaxRows;
   uint32_t* d_colmax = (uint32_t*)at(L.off_colmax);
   uint32_t* d_zcolmax = (uint32_t*)at(L.off_zcolmax);
@@ -1028,7 +1025,7 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
   bool colmax_ready = false;
   bool near_switch = false;  // counters[3] of the last solve
   // DLSA_OZ_ZREC=0 (A/B only): no max |z| records, every exponent from max |x| / 2
-  const bool zrec = !(getenv("DLSA_OZ_ZREC") && atoi(getenv("DLSA_OZ_ZREC")) == 0);
+  const bool zrec = !(env_knob("DLSA_OZ_ZREC") && atoi(env_knob("DLSA_OZ_ZREC")) == 0);
   if (use_oz) {
     DLSA_HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)d_zcolmax, 0x7F800000u,
                                    (size_t)std::max(pl.n_chunks, 1) * pl.PP, stream));
@@ -1278,7 +1275,7 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
   // profiles/r04n_cat_warm_start_ab.txt).  DLSA_WARM_START overrides.
   std::vector<Plan> plans;
   opt.warm_start = opt.warm_start && K > 0 && n_total / K >= (int64_t(1) << 19);
-  if (const char* e = getenv("DLSA_WARM_START")) opt.warm_start = atoi(e);
+  if (const char* e = env_knob("DLSA_WARM_START")) opt.warm_start = atoi(e);
   if (opt.warm_start) {
     const int64_t min_rows = std::max<int64_t>(2048, 64LL * P);
     for (double frac : warm_level_fracs(true)) {

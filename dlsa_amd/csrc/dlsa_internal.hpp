@@ -80,7 +80,23 @@ struct PassArgs {
   uint32_t* colmax;
   uint32_t* zcolmax;
   const double* theta_rec;
+  int32_t waves;  // fp64 per-wave pass geometry (dlsa_fit_options.exact_waves; 0 = auto)
 };
+
+// A/B knobs of profiling builds.  The product library reads no environment
+// variable that changes a result (include/dlsa_hip.h): env_knob() is getenv
+// only in builds compiled with -DDLSA_ENV_KNOBS=1 (tools/build_variants.sh).
+#ifndef DLSA_ENV_KNOBS
+#define DLSA_ENV_KNOBS 0
+#endif
+inline const char* env_knob(const char* name) {
+#if DLSA_ENV_KNOBS
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
 
 // Arguments of the per-partition Newton update.
 struct SolveArgs {

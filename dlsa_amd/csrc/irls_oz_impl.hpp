@@ -77,6 +77,23 @@ constexpr int RB = 32;           // rows per DMA block
 constexpr int RPW = RB / NPW;    // rows per producer wave per block (8)
 constexpr int LPR = 64 / RPW;    // row-phase lanes per row (8)
 constexpr int NSLOT = 6;         // ring: 2 in flight, 2 producing, 2 consuming
+// Ring-slot ownership.  Between barriers B_m and B_{m+1}:
+//   slots of blocks 2m+2, 2m+3: written only by the LDS-DMA (issued by the
+//     consumers), read by nobody;
+//   slots of blocks 2m, 2m+1: producer wave pw reads and then overwrites
+//     ONLY the bytes of its own 8 rows (rows 8 pw .. 8 pw + 7 of each block)
+//     -- there is no barrier between one producer wave's reads and another's
+//     image stores, so a value read from another wave's rows may already be
+//     digit bytes (the padding features f >= P of row 8 pw + 7 read row
+//     8 pw + 8 and are zeroed, never used);
+//   slots of blocks 2m-2, 2m-1: read only (the consumers' operands).
+// DLSA_OZ_CHECK builds poison (NaN) any producer read of a feature f < P
+// outside the reading wave's own rows, so a violation ends the partition
+// nonfinite in the tests.
+static_assert(NSLOT >= 6, "2 blocks in flight + 2 producing + 2 consuming");
+#ifndef DLSA_OZ_CHECK
+#define DLSA_OZ_CHECK 0
+#endif
 // digits per value (DLSA_OZ_DIGITS: 5, the product; 4: a 30-bit grid, levels
 // 0-4 -- 8 MFMAs per tile and 32-row block instead of 9, one quad transpose
 // per value; ~5e-11 instead of ~2e-12 per entry in the numpy restatement; A/B
@@ -698,13 +715,16 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
       left[X] = nrows - b * RB;
     }
     // ---- row phase of both blocks: 8 rows per wave, 8 lanes per row ---------
-    // Two full blocks (every block but a chunk's last) read x unmasked: a
-    // feature f >= P of a row reads the row's successor in the same block (or,
-    // for the block's last row, the slot's y bytes): finite values of this
-    // chunk that meet beta_f = 0 in eta, and whose gradient and H entries the
-    // solve never reads (f >= P).  A chunk's last block(s) zero the rows past
-    // the chunk (they hold the next partition's rows, which must not leak
-    // into this one, not even as NaN) and the padding features.
+    // Two full blocks (every block but a chunk's last) need no row mask.  The
+    // padding features f >= P of a row are still zeroed: their x reads land
+    // on the row's successor, and the successor of a wave's last row (row
+    // 8 pw + 7) is the first row of producer wave pw + 1, which overwrites
+    // those bytes with its digit image as soon as it has read them -- with no
+    // barrier in between, so the bytes read here may be digit bytes, i.e. any
+    // double including NaN / inf, and NaN * beta_f (= 0) is NaN (ring-slot
+    // ownership rule).  A chunk's last block(s) also zero the
+    // rows past the chunk (they hold the next partition's rows, which must
+    // not leak into this one, not even as NaN).
     const bool full = left[0] >= RB && left[1] >= RB;  // workgroup-uniform
     double xv[2][M], e[2], r[2];
     auto row_phase = [&](auto maskI) {
@@ -718,13 +738,23 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
         for (int m2 = 0; m2 < M; ++m2) {
           const int f = sl + LPR * m2;
           double v = xr[LPR * m2];
+          if constexpr (DLSA_OZ_CHECK) {  // ownership rule: own rows for f < P
+            const int e = rB * p + f - ic;  // element of the block this lane reads
+            // a violation poisons the row (the partition ends nonfinite: the
+            // tests see it without a fault)
+            if (f >= ic && f < P && (e < pw * RPW * p || e >= (pw + 1) * RPW * p))
+              v = __builtin_nan("");
+          }
           if constexpr (STD) v = (v - stdv[f]) * stdv[PMAX + f];
           if (m2 == 0 && ic && sl == 0) v = 1.0;
-          if constexpr (MASK) {
-            // features below the smallest P of this NT are always < P
-            const bool fin = LPR * m2 + LPR - 1 < 16 * (NT - 1) + 1 || ((fmask >> m2) & 1u);
+          // features below the smallest P of this NT are always < P
+          // (compile-time for all but the last one or two m2)
+          const bool always_in = LPR * m2 + LPR - 1 < 16 * (NT - 1) + 1;
+          const bool fin = always_in || ((fmask >> m2) & 1u);
+          if constexpr (MASK)
             v = (valid && fin) ? v : 0.0;
-          }
+          else
+            v = fin ? v : 0.0;
           xv[X][m2] = v;
           if (m2 & 1)
             e1 = fma(v, beta[m2], e1);

@@ -675,11 +675,10 @@ __global__ __launch_bounds__(64 * W, wave_min_waves(NT, W, FAM)) void irls_wave_
   }
 }
 
-static inline int wave_w(int NT) {
-  if (const char* e = getenv("DLSA_WAVE_W")) {
-    const int w = atoi(e);
-    if ((w == 1 && NT <= 8) || (w == 2 && NT >= 2 && NT <= 7)) return w;
-  }
+// requested: dlsa_fit_options.exact_waves (0 = automatic)
+static inline int wave_w(int NT, int requested = 0) {
+  const int w = requested;
+  if ((w == 1 && NT <= 8) || (w == 2 && NT >= 2 && NT <= 7)) return w;
   return wave_w_default(NT);
 }
 
@@ -705,7 +704,7 @@ static hipError_t launch_wave_t(const PassArgs& a, int n_chunks, hipStream_t s) 
 template <int NT, bool STD, int FAM>
 static hipError_t launch_wave_sf(const PassArgs& a, int n_chunks, hipStream_t s) {
   if constexpr (NT >= 2 && NT <= 7) {
-    if (wave_w(NT) == 2) return launch_wave_t<NT, 2, STD, FAM>(a, n_chunks, s);
+    if (wave_w(NT, a.waves) == 2) return launch_wave_t<NT, 2, STD, FAM>(a, n_chunks, s);
   }
   return launch_wave_t<NT, 1, STD, FAM>(a, n_chunks, s);
 }

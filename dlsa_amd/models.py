@@ -282,7 +282,7 @@ class BatchedFit:
 def logistic_model_batched(X, y, offsets, fit_intercept=False, center=None, scale=None,
                            max_iter=100, tol=1e-10, hessian="mixed", switch_tol=1e-6,
                            record_timing=False, rows_per_chunk=0, workspace=None,
-                           device=None):
+                           device=None, exact="auto", exact_waves=0, oz_max_bytes=0):
     """Fit K row partitions at once on the GPU (batched Newton/IRLS).
 
     Per partition k (rows ``offsets[k]:offsets[k+1]`` of X) this computes what
@@ -296,7 +296,12 @@ def logistic_model_batched(X, y, offsets, fit_intercept=False, center=None, scal
     y: [n] 0/1; offsets: K+1 host ints.  ``hessian`` = "mixed" (bf16-MFMA
     Hessian until the Newton step is below ``switch_tol``, then fp64-MFMA
     passes; the gradient and the returned Sig_inv are always fp64),
-    "mixed_f32" (fp32-MFMA approximate Hessian) or "fp64".
+    "mixed_f32" (fp32-MFMA approximate Hessian) or "fp64".  ``exact`` =
+    "auto" (the exact pass that publishes Sig_inv on the int8 matrix cores,
+    as int8 digit slices, wherever it applies; ~1e-12 per entry) or "fp64"
+    (fp64 MFMA); ``exact_waves`` (0, 1, 2) the fp64 exact pass's geometry
+    for P <= 128 and ``oz_max_bytes`` a cap on the wide path's int8 digit
+    records (include/dlsa_hip.h, dlsa_fit_options).
     """
     dev = _require_gpu(device)
     Xd = _dev_f64(X, dev)
@@ -333,6 +338,9 @@ def logistic_model_batched(X, y, offsets, fit_intercept=False, center=None, scal
     opt.switch_tol = float(switch_tol)
     opt.record_timing = 1 if record_timing else 0
     opt.rows_per_chunk = int(rows_per_chunk)
+    opt.exact_pass = {"auto": _hip.EXACT_AUTO, "fp64": _hip.EXACT_FP64}[exact]
+    opt.exact_waves = int(exact_waves)
+    opt.oz_max_bytes = int(oz_max_bytes)
     offs_p = offs.ctypes.data_as(ctypes.c_void_p)
     need = lib.dlsa_logistic_workspace_bytes(offs_p, K, p, int(bool(fit_intercept)),
                                              opt.rows_per_chunk)
@@ -424,7 +432,7 @@ def logistic_model_batched_categorical(Xn, codes, y, offsets, levels, fit_interc
 
 
 def ols_model_batched(X, y, offsets, fit_intercept=False, center=None, scale=None,
-                      rows_per_chunk=0, record_timing=False, device=None):
+                      rows_per_chunk=0, record_timing=False, device=None, exact_waves=0):
     """Batched local OLS (linear DLSA path): per
     partition theta_k = (X_k^T X_k)^-1 X_k^T y_k and Sig_inv_k = X_k^T X_k from
     one fused fp64 pass.  Returns a BatchedFit whose ``loglik`` field holds the
@@ -453,6 +461,7 @@ def ols_model_batched(X, y, offsets, fit_intercept=False, center=None, scale=Non
     opt = _hip.default_options()
     opt.rows_per_chunk = int(rows_per_chunk)
     opt.record_timing = 1 if record_timing else 0
+    opt.exact_waves = int(exact_waves)
     rc = lib.dlsa_ols_fit_batched(_ptr(Xd), _ptr(yd), offs.ctypes.data_as(ctypes.c_void_p), K, p,
                                   int(bool(fit_intercept)), _ptr(cd), _ptr(sd), _ptr(theta),
                                   _ptr(sig), _ptr(sigt), _ptr(rss), _ptr(status),

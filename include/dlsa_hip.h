@@ -63,17 +63,34 @@ extern "C" {
                                         all-zero frame (models.py:84-91) */
 
 /* Hessian arithmetic of the Newton passes.  The gradient, eta, the weights
- * and the returned log-likelihood and Sig_inv are fp64 in every mode; the
- * approximate Hessians only steer Newton (the fp64 gradient fixes the
- * solution). */
+ * and the returned log-likelihood are fp64 in every mode; the approximate
+ * Hessians only steer Newton (the fp64 gradient fixes the solution).  The
+ * Hessian returned as Sig_inv comes from the EXACT pass(es) that end the fit,
+ * whose arithmetic dlsa_fit_options.exact_pass selects (DLSA_EXACT_*). */
 #define DLSA_HESSIAN_MIXED 0      /* bf16 MFMA Hessian until the step is below
-                                     switch_tol, then fp64 MFMA pass(es); a
-                                     partition whose step stops shrinking (two
-                                     iterations in a row without halving, or
-                                     backtracking) moves to fp32 MFMA, then fp64 */
-#define DLSA_HESSIAN_FP64 1       /* fp64 MFMA Hessian on every pass */
+                                     switch_tol, then exact pass(es); a partition
+                                     whose step stops shrinking (two iterations
+                                     in a row without halving, or backtracking)
+                                     moves to fp32 MFMA, then to exact passes */
+#define DLSA_HESSIAN_FP64 1       /* fp64 MFMA Hessian on every pass (exact_pass is
+                                     ignored) */
 #define DLSA_HESSIAN_MIXED_F32 2  /* as MIXED with fp32 MFMA approximate passes
                                      (for ill-conditioned designs) */
+
+/* Arithmetic of the exact pass in the MIXED modes.
+ * DLSA_EXACT_AUTO: X^T W X from int8 digit slices on the int8 matrix cores
+ *   (the Ozaki scheme) wherever it applies -- P <= 112 with chunks of at most
+ *   32767 rows, and P > DLSA_MAX_P_FUSED when the workspace holds the digit
+ *   records -- otherwise fp64 MFMA.  z = sqrt(w) x is rounded to a 38-bit
+ *   fixed-point grid below 2^E_f per chunk (or row group) and feature, the
+ *   digit products are summed exactly in int32 and the levels below 2^-40 of
+ *   the leading product are dropped: every entry of Sig_inv is within about
+ *   1e-12 sqrt(H_ii H_jj) of the fp64 sum (tests/test_gpu_ozaki.py pins
+ *   < 1e-10 on heavy-tailed designs), and the result is bit-identical run to
+ *   run.  The logistic weights, gradient, log-likelihood and theta stay fp64.
+ * DLSA_EXACT_FP64: every exact pass on the fp64 MFMA (v_mfma_f64_16x16x4). */
+#define DLSA_EXACT_AUTO 0
+#define DLSA_EXACT_FP64 1
 
 #define DLSA_MAX_P_FUSED 192  /* largest P handled by the fused pass + LDS Newton solve */
 #define DLSA_MAX_P 512        /* largest P overall: above DLSA_MAX_P_FUSED a row pass, a
@@ -98,8 +115,19 @@ typedef struct dlsa_fit_options {
                                (a level takes at most half of what is left), so
                                iters[k] <= max_iter and max_iter = 1 is one
                                full-data Newton step from 0 */
-  int32_t reserved[6];
+  int32_t exact_pass;       /* DLSA_EXACT_AUTO (default) or DLSA_EXACT_FP64 */
+  int32_t exact_waves;      /* geometry of the fp64 exact pass for P <= 128: 0 =
+                               automatic, 1 = all tiles in one wave, 2 = two waves
+                               (P 17..112); the result does not depend on it */
+  int64_t oz_max_bytes;     /* P > DLSA_MAX_P_FUSED, mixed mode: at most this many
+                               bytes of int8 digit records (<= 0: no cap); more
+                               runs the fp64 Gram (dlsa_fit_stats.oz_fallbacks) */
+  int32_t reserved[2];
 } dlsa_fit_options;
+/* The library reads no environment variable that changes a result: the
+ * output of every entry point depends only on its arguments.  (DLSA_TRACE
+ * prints per-iteration steps to stderr; profiling builds compiled with
+ * -DDLSA_ENV_KNOBS=1 also read the A/B knobs named in capi.hip.) */
 
 typedef struct dlsa_fit_stats {
   int32_t iterations;       /* Newton iterations run (max over partitions) */
@@ -128,7 +156,7 @@ typedef struct dlsa_fit_stats {
                                digit records had no room (a workspace of at least
                                the size without them but smaller than
                                dlsa_logistic_workspace_bytes, a failed
-                               allocation, or DLSA_WIDE_OZ_MAX_BYTES) */
+                               allocation, or dlsa_fit_options.oz_max_bytes) */
 } dlsa_fit_stats;
 
 /* Default options (mixed Hessian, automatic chunking, no timing). */
@@ -229,7 +257,12 @@ int dlsa_logistic_loglik_batched(const double* X, const double* y,
  * Parameters (P = fit_intercept + q + sum_f (levels[f] - 1) <= DLSA_MAX_P_FUSED):
  *   [intercept] [numeric 0..q-1] [factor 0 dummies 1..L0-1] [factor 1 ...] ...
  * The one-hot blocks of X^T W X are computed as weighted histograms in LDS
- * (exact fp64); outputs are as in dlsa_logistic_fit_batched (theta,
+ * with int64 fixed-point bins: each term w, w x_i, y - mu is rounded once to
+ * a power-of-two grid chosen per partition and column from the partition's
+ * own max |x_i| (so that no bin can overflow), then summed exactly --
+ * bit-identical run to run and within ~1e-13 of an fp64 sum relative to the
+ * column's scale; the numeric x numeric block is fp64.  Outputs are as in
+ * dlsa_logistic_fit_batched (theta,
  * Sig_inv = X^T W X of the dummy-expanded design at theta, ...).  A partition
  * in which some dummy column has no rows gets DLSA_STATUS_MISSING_LEVEL and
  * all-zero outputs, the reference's "fake zero matrix".  Codes >= levels[f]

@@ -5,7 +5,7 @@ In mixed mode every full-data bf16 pass records, per chunk and feature, max
 Sig_inv (models.py:130) then forms X^T W X from int8 digit slices with exact
 int32 sums, its digit exponents from that record (grown by the bound on how
 far sqrt(w) can have moved since).  The same fit
-with DLSA_OZ=0 runs the fp64-MFMA exact pass at the SAME iterate (the bf16
+with exact="fp64" (DLSA_EXACT_FP64) runs the fp64-MFMA exact pass at the SAME iterate (the bf16
 passes are deterministic), so the two Sig_inv differ only by the Ozaki
 scheme's error: asserted below 1e-11 relative to the largest entry (the
 path's tolerance is 1e-8), per diagonal entry below 1e-10 of its own size on
@@ -88,12 +88,10 @@ def heavy_design(kind, n, chunk=4096, seed=0, p_extra=0):
 
 
 def _pair(M, monkeypatch, *args, **kw):
-    """The same fit with the Ozaki exact pass and with the fp64-MFMA one."""
-    monkeypatch.delenv("DLSA_OZ", raising=False)
-    oz = M.logistic_model_batched(*args, **kw)
-    monkeypatch.setenv("DLSA_OZ", "0")
-    f64 = M.logistic_model_batched(*args, **kw)
-    monkeypatch.delenv("DLSA_OZ", raising=False)
+    """The same fit with the Ozaki exact pass and with the fp64-MFMA one
+    (dlsa_fit_options.exact_pass)."""
+    oz = M.logistic_model_batched(*args, exact="auto", **kw)
+    f64 = M.logistic_model_batched(*args, exact="fp64", **kw)
     return oz, f64
 
 
@@ -307,7 +305,8 @@ def test_wide_ozaki_concurrent_fits_two_threads(torch_cuda, M):
         assert torch.equal(out[p].loglik, seq[p].loglik)
 
 
-def _abi_fit(torch, X, y, off, p, workspace_bytes, guard=0, pattern=0xA5, rows_per_chunk=2000):
+def _abi_fit(torch, X, y, off, p, workspace_bytes, guard=0, pattern=0xA5, rows_per_chunk=2000,
+             oz_max_bytes=0):
     """dlsa_logistic_fit_batched_ex through ctypes with a caller workspace of
     exactly `workspace_bytes` (plus `guard` bytes of `pattern` after it, or a
     NULL workspace when workspace_bytes is None)."""
@@ -327,6 +326,7 @@ def _abi_fit(torch, X, y, off, p, workspace_bytes, guard=0, pattern=0xA5, rows_p
     st = torch.empty(K, dtype=torch.int32, device="cuda")
     opt = _hip.default_options()
     opt.rows_per_chunk = rows_per_chunk
+    opt.oz_max_bytes = oz_max_bytes
     ws = None
     if workspace_bytes is not None:
         ws = torch.full((workspace_bytes + guard,), pattern, dtype=torch.uint8, device="cuda")
@@ -348,7 +348,7 @@ def test_wide_ozaki_workspace_ownership_and_fallback(torch_cuda, M, monkeypatch)
     nothing past its end (a guard band of 1 MiB keeps its fill pattern); one
     byte less cannot hold the records and runs the fp64 Gram (oz_fallbacks =
     1, no error); a NULL workspace is allocated and freed inside the call;
-    DLSA_WIDE_OZ_MAX_BYTES below the records' size falls back the same way."""
+    dlsa_fit_options.oz_max_bytes below the records' size falls back the same way."""
     import ctypes
 
     torch = torch_cuda
@@ -371,9 +371,7 @@ def test_wide_ozaki_workspace_ownership_and_fallback(torch_cuda, M, monkeypatch)
     th_n, S_n, st_n, _ = _abi_fit(torch, X, y, off, p, None)
     assert st_n["passes_oz"] >= 1 and st_n["oz_fallbacks"] == 0
     assert torch.equal(th_n, th) and torch.equal(S_n, S)
-    monkeypatch.setenv("DLSA_WIDE_OZ_MAX_BYTES", "4096")
-    th_c, S_c, st_c, _ = _abi_fit(torch, X, y, off, p, need)
-    monkeypatch.delenv("DLSA_WIDE_OZ_MAX_BYTES")
+    th_c, S_c, st_c, _ = _abi_fit(torch, X, y, off, p, need, oz_max_bytes=4096)
     assert st_c["passes_oz"] == 0 and st_c["oz_fallbacks"] == 1
     assert torch.equal(th_c, th_f) and torch.equal(S_c, S_f)
     thr, Sr, _, _, _ = O.logistic_fit_partitions(X, y, off)

@@ -740,11 +740,10 @@ def test_hessian_mixed_f32_vs_oracle(torch_cuda, M, p, fi):
 @pytest.mark.parametrize("p,fi,std", [(17, False, False), (64, True, True), (100, False, False),
                                       (111, True, False)])
 def test_exact_pass_wave_split_vs_oracle(torch_cuda, M, monkeypatch, w, p, fi, std):
-    """The per-wave exact pass in both geometries (DLSA_WAVE_W: all tiles in
+    """The per-wave exact pass in both geometries (exact_waves: all tiles in
     one wave, or the tile rows split over two waves with the rows of a block
     split in the row phase): fp64 fits and OLS against the oracle, with
     standardisation, intercept and ragged partitions (block tails)."""
-    monkeypatch.setenv("DLSA_WAVE_W", w)
     sizes = [3001, 1777, 4096 + 9]
     n = sum(sizes)
     X, y = O.simulate_counter(n, p, seed=3 * p + fi)
@@ -754,7 +753,7 @@ def test_exact_pass_wave_split_vs_oracle(torch_cuda, M, monkeypatch, w, p, fi, s
         center, scale = X.mean(0), X.std(0)
     off = np.concatenate([[0], np.cumsum(sizes)])
     fit = M.logistic_model_batched(X, y, off, fit_intercept=fi, center=center, scale=scale,
-                                   hessian="fp64", rows_per_chunk=1000)
+                                   hessian="fp64", rows_per_chunk=1000, exact_waves=int(w))
     th, S, St, ll, it = O.logistic_fit_partitions(X, y, off, fit_intercept=fi, center=center,
                                                   scale=scale)
     assert (fit.status.cpu().numpy() == 0).all()
@@ -762,7 +761,8 @@ def test_exact_pass_wave_split_vs_oracle(torch_cuda, M, monkeypatch, w, p, fi, s
     assert _rel(fit.sig_inv.cpu(), S) < REL
     assert _rel(fit.loglik.cpu(), ll) < 1e-10
     yl = X[:, :3].sum(1) + 0.1 * y
-    ols = M.ols_model_batched(X, yl, off, fit_intercept=fi, rows_per_chunk=1000)
+    ols = M.ols_model_batched(X, yl, off, fit_intercept=fi, rows_per_chunk=1000,
+                              exact_waves=int(w))
     for k in range(3):
         o = O.ols_fit(X[off[k]:off[k + 1]], yl[off[k]:off[k + 1]], fit_intercept=fi)
         assert _rel(ols.theta[k].cpu(), o["coef"]) < REL

@@ -1,8 +1,8 @@
 #!/bin/bash
 # Profiling-only builds of libdlsa_hip.so with DLSA_ABLATE=1/2/3 (see
-# dlsa_amd/csrc/irls_coop_impl.hpp; nt / sc1: cache policy of the X stream).  Output: tools/_variants/*.so (git-ignored).
+# dlsa_amd/csrc/irls_coop_impl.hpp; nt / sc1: cache policy of the X stream).  Output: var/*.so (git-ignored, travels to the GPU box).
 set -e
-mkdir -p tools/_variants
+mkdir -p var
 cd "$(dirname "$0")/.."
 for v in "$@"; do
   case $v in
@@ -25,6 +25,8 @@ for v in "$@"; do
     olsr3) D="DLSA_WAVE_NSLOT_OLS=2 -DDLSA_WAVE_OLS_ONESYNC=0" ;;
     word) D=DLSA_WAVE_ORDER=1 ;;
     ozprof) D=DLSA_OZ_PROF=1 ;;
+    ozcheck) D=DLSA_OZ_CHECK=1 ;;
+    knobs) D=DLSA_ENV_KNOBS=1 ;;
     ozs1) D=DLSA_OZ_SCHED=1 ;;
     oz4d) D="DLSA_OZ_DIGITS=4 -DDLSA_OZ_DBATCH=0" ;;
     oz4dprof) D="DLSA_OZ_DIGITS=4 -DDLSA_OZ_DBATCH=0 -DDLSA_OZ_PROF=1" ;;
@@ -55,5 +57,5 @@ for v in "$@"; do
     oz*|ozs*) ONLY='["irls_oz.hip", "irls_oz_g2.hip"]' ;;
     ols*|wslot3) ONLY='["irls_wave.hip", "irls_wave_g2.hip"]' ;;
   esac
-  python -c "from dlsa_amd.build import build; print(build(force=True, out='tools/_variants/libdlsa_hip_$v.so', defines='$D'.replace('-D', '').split(), only=$ONLY))"
+  python -c "from dlsa_amd.build import build; print(build(force=True, out='var/libdlsa_hip_$v.so', defines='$D'.replace('-D', '').split(), only=$ONLY))"
 done
