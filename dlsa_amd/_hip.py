@@ -103,6 +103,7 @@ SIGNATURES = {
     "dlsa_last_fit_stats": (ctypes.c_int, [ctypes.POINTER(FitStats)]),
     "dlsa_reduce_partitions": (ctypes.c_int, [_P, _P, _P, _I32, _I32, _P, _P]),
     "dlsa_simulate_logistic": (ctypes.c_int, [_P, _P, _I64, _I32, ctypes.c_uint64, _I64, _P]),
+    "dlsa_column_moments": (ctypes.c_int, [_P, _I64, _I32, _P, _P]),
     "dlsa_lars_lsa": (ctypes.c_int, [_P, _P, _I32, _I32, _F64, _I32, _F64, _I32, _P, _P, _P,
                                      _P, _P]),
     "dlsa_last_error": (ctypes.c_char_p, []),

@@ -1300,7 +1300,8 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
   const int64_t off_bad = align_up(off_counts + 4LL * std::max(pl.n_chunks, 1) * std::max(D, 1), 256);
   const int64_t off_badp = align_up(off_bad + 4LL * std::max(pl.n_chunks, 1), 256);
   const int64_t off_colmax = align_up(off_badp + 4LL * K, 256);
-  const int64_t total = align_up(off_colmax + 8LL * kCatQMax * std::max(pl.n_chunks, 1), 256);
+  const int64_t off_hs = align_up(off_colmax + 8LL * kCatQMax * std::max(pl.n_chunks, 1), 256);
+  const int64_t total = align_up(off_hs + 8LL * (kCatQMax + 2) * K, 256);
   g_stats.n_chunks = pl.n_chunks;
 
   char* ws = (char*)opt.workspace;
@@ -1331,6 +1332,7 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
   int32_t* d_bad = (int32_t*)at(off_bad);
   int32_t* d_badp = (int32_t*)at(off_badp);
   double* d_colmax = (double*)at(off_colmax);
+  double* d_hs = (double*)at(off_hs);
 
   auto upload = [&](const Plan& qn) -> hipError_t {
     hipError_t e = hipSuccess;
@@ -1385,6 +1387,7 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
   }
   DLSA_HIP_TRY(hipMemcpyAsync(h_phase.data(), d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
   DLSA_HIP_TRY(hipStreamSynchronize(stream));
+  std::vector<double> h_hs;  // the grids (alive until the fit's next stream sync)
   {
     // fixed-point grids: 2^E with |term| * 2^E * max(rows of a chunk, 1024) <= 2^60,
     // so a bin's sum stays in int64 and every term below 2^50 (the kernel's
@@ -1397,19 +1400,30 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
       const int e = (int)std::floor(60.0 - std::log2(bound * (double)rmax));
       return std::ldexp(1.0, std::max(-900, std::min(900, e)));
     };
-    ca.hscale[0] = grid(0.25);  // w = mu (1 - mu) <= 1/4; pair cells
-    ca.hscale[1] = grid(1.0);   // |y - mu| <= 1
+    // per partition (its chunks of the full plan cover all its rows, so the
+    // bound holds for every warm-start level's chunks too): an outlier row
+    // coarsens only its own partition's grid
     std::vector<double> hc(q, 0.0), hs(q, 1.0);
     if (center && q > 0) {  // the kernel sums w (x - c) / s
       DLSA_HIP_TRY(hipMemcpy(hc.data(), center, 8LL * q, hipMemcpyDeviceToHost));
       DLSA_HIP_TRY(hipMemcpy(hs.data(), scale, 8LL * q, hipMemcpyDeviceToHost));
     }
-    for (int j = 0; j < q; ++j) {
-      double m = 0.0;
-      for (int c = 0; c < pl.n_chunks; ++c) m = std::max(m, h_colmax[(size_t)c * kCatQMax + j]);
-      if (center) m = (m + std::fabs(hc[j])) / std::fabs(hs[j]);
-      ca.hscale[2 + j] = grid(0.25 * m);
+    h_hs.assign((size_t)K * (kCatQMax + 2), 1.0);
+    for (int k = 0; k < K; ++k) {
+      double* o = h_hs.data() + (size_t)k * (kCatQMax + 2);
+      o[0] = grid(0.25);  // w = mu (1 - mu) <= 1/4; pair cells
+      o[1] = grid(1.0);   // |y - mu| <= 1
+      for (int j = 0; j < q; ++j) {
+        double m = 0.0;
+        for (int c = pl.part_chunk_begin[k]; c < pl.part_chunk_begin[k + 1]; ++c)
+          m = std::max(m, h_colmax[(size_t)c * kCatQMax + j]);
+        if (center) m = (m + std::fabs(hc[j])) / std::fabs(hs[j]);
+        o[2 + j] = grid(0.25 * m);
+      }
     }
+    DLSA_HIP_TRY(hipMemcpyAsync(d_hs, h_hs.data(), 8LL * (kCatQMax + 2) * K,
+                                hipMemcpyHostToDevice, stream));
+    ca.hscale = d_hs;
   }
   for (int k = 0; k < K; ++k)
     if (h_badp[k]) {
@@ -1742,6 +1756,25 @@ int dlsa_reduce_partitions(const double* sig_inv, const double* sig_inv_theta,
   }
   DLSA_HIP_TRY(launch_reduce_partitions(sig_inv, sig_inv_theta, theta, K, p, out,
                                         (hipStream_t)stream));
+  return DLSA_OK;
+}
+
+int dlsa_column_moments(const double* X, int64_t n, int32_t p, double* out, void* stream_) {
+  g_last_error.clear();
+  if (n < 0 || p < 1 || (n > 0 && !X) || !out) {
+    set_error("dlsa_column_moments: invalid arguments");
+    return DLSA_E_INVALID;
+  }
+  hipStream_t stream = (hipStream_t)stream_;
+  int G = 1;
+  int64_t rpr = 1;
+  column_moments_plan(n, p, &G, &rpr);
+  double* ws = nullptr;
+  DLSA_HIP_TRY(hipMallocAsync((void**)&ws, sizeof(double) * (5LL * G + 5) * p, stream));
+  const hipError_t e = launch_column_moments(X, n, p, out, ws, G, rpr, stream);
+  const hipError_t f = hipFreeAsync(ws, stream);
+  DLSA_HIP_TRY(e);
+  DLSA_HIP_TRY(f);
   return DLSA_OK;
 }
 

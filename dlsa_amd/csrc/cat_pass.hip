@@ -15,9 +15,10 @@
 //   gradient dummy (f,l)         sum_{code_f = l} (y - mu)
 //
 // The histogram bins are 64-bit FIXED-POINT integers (ds_add_u64): each term
-// is rounded once to a power-of-two grid chosen per column from the data's
-// range (scale 2^E with 0.25 max|x| 2^E x rows-per-chunk <= 2^61, so no bin
-// can overflow; for config 3 the grid step is ~1e-14 of the column's range),
+// is rounded once to a power-of-two grid chosen per partition and column from
+// the partition's own range (scale 2^E with 0.25 max|x| 2^E x rows-per-chunk
+// <= 2^61, so no bin can overflow; for config 3 the grid step is ~1e-14 of the
+// column's range; an outlier row coarsens only its own partition's grid),
 // then integer addition is exact and order-free -- the result is bit-identical
 // run to run whatever order the hardware applies the atomics in, and within
 // ~1e-13 relative of an fp64 sum.  The dense blocks (numeric x numeric,
@@ -123,7 +124,9 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
   // inside the row loop): [0] w, [1] residual, [2 + i - ic] w x_i
   double hsc[QN + 2];
 #pragma unroll
-  for (int i = 0; i < QN + 2; ++i) hsc[i] = (i < 2 + q && i < kCatQMax + 2) ? a.hscale[i] : 0.0;
+  for (int i = 0; i < QN + 2; ++i)
+    hsc[i] = (i < 2 + q && i < kCatQMax + 2) ? a.hscale[(int64_t)part * (kCatQMax + 2) + i] : 0.0;
+  const double* hs = a.hscale + (int64_t)part * (kCatQMax + 2);  // the epilogue's
   double hacc[NTRI], gacc[QN], llacc = 0.0;
 #pragma unroll
   for (int i = 0; i < NTRI; ++i) hacc[i] = 0.0;
@@ -259,7 +262,7 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
     long long s = 0;
     for (int rp = 0; rp < R; ++rp)
       s += hist_at(hist, a.nd_off[f] + (rp * nl + lev) * a.nd_stride + col);
-    return (double)s / (col == 0 ? a.hscale[0] : a.hscale[1 + col]);
+    return (double)s / (col == 0 ? hs[0] : hs[1 + col]);
   };
 
   // ---- epilogue: the partial slab in the dense pass's tile format ---------
@@ -291,7 +294,7 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
             const int nli = a.nlev[fi], nlj = a.nlev[fj], R = a.pr_rep[pi];
             long long s = 0;
             for (int rp = 0; rp < R; ++rp) s += hist_at(hist, a.pr_off[pi] + (rp * nlj + lj) * nli + li);
-            v = (double)s / a.hscale[0];
+            v = (double)s / hs[0];
           }
         }
       }
@@ -309,61 +312,103 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
       const int nl = a.nlev[f], R = a.nd_rep[f];
       long long s = 0;
       for (int rp = 0; rp < R; ++rp) s += hist_at(hist, a.g_off[f] + rp * nl + l);
-      v = (double)s / a.hscale[1];
+      v = (double)s / hs[1];
     }
     a.slab_g[(int64_t)chunk * PP + e] = v;
   }
   if (tid == 0) a.slab_ll[chunk] = fin[NTRI + QN];
 }
 
-// Level presence per chunk: counts[chunk, d] = rows of the chunk whose code
-// selects dummy column d; bad[chunk] = codes outside 0..L_f-1; colmax[chunk, i]
-// = max |x_i| over the chunk (raw numeric columns: the fixed-point grids).
+// Level presence per chunk: counts[chunk, d] = 1 if a row of the chunk
+// selects dummy column d (presence flags: plain LDS stores of 1, no atomics);
+// bad[chunk] = codes outside 0..L_f-1; colmax[chunk, i] = max |x_i| over the
+// finite values of the chunk (raw numeric columns: the fixed-point grids).
+// One streaming read of the chunk's codes and numeric columns with
+// wave-contiguous loads: each wave takes windows of F dwords (q doubles) per
+// lane, so the factor of every code byte (the column of every value) is
+// fixed per lane and load slot -- the maxima stay in registers until one LDS
+// max per lane and slot (|x| >= 0 orders like its bits as uint64).
 __global__ __launch_bounds__(256) void cat_presence_kernel(const CatArgs a, int32_t* counts,
                                                            int32_t* bad, double* colmax) {
-  __shared__ int32_t cnt[kCatPMax + 1];
-  __shared__ double cmax[4][kCatQMax];
-  const int chunk = blockIdx.x, tid = threadIdx.x;
-  const int D = a.P - a.intercept - a.q;
-  const int F = a.F;
-  for (int i = tid; i <= kCatPMax; i += 256) cnt[i] = 0;
+  __shared__ int32_t flag[kCatPMax];
+  __shared__ int32_t nbad;
+  __shared__ unsigned long long cmax[kCatQMax];
+  __shared__ int32_t t_nlev[kCatMaxFactors], t_doff[kCatMaxFactors];
+  const int chunk = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int F = a.F, q = a.q;
+  const int D = a.P - a.intercept - q;
+  const int doff0 = a.intercept + q;
+  for (int i = tid; i < kCatPMax; i += 256) flag[i] = 0;
+  if (tid < kCatQMax) cmax[tid] = 0ull;
+  if (tid < kCatMaxFactors) {
+    t_nlev[tid] = a.nlev[tid];
+    t_doff[tid] = a.doff[tid] - doff0;
+  }
+  if (tid == 0) nbad = 0;
   __syncthreads();
   const int64_t row0 = a.chunk_row0[chunk];
   const int nrows = a.chunk_rows[chunk];
-  const int doff0 = a.intercept + a.q;
-  double mx[kCatQMax];
+
+  // ---- codes: bytes [row0 F, (row0 + nrows) F), read as aligned dwords -----
+  if (F > 0) {
+    const uintptr_t cb = (uintptr_t)(a.codes + row0 * F);
+    const uintptr_t base = cb & ~(uintptr_t)3;
+    const int skew = (int)(cb - base);
+    const int64_t nbytes = (int64_t)nrows * F;
+    const int64_t wstride = 4LL * F * 256;  // bytes per workgroup iteration (a multiple of F)
+    int nb = 0;
+    for (int64_t o0 = (int64_t)wid * F * 256; o0 < skew + nbytes; o0 += wstride) {
+      for (int s = 0; s < F; ++s) {
+        const int64_t o = o0 + s * 256 + 4 * lane;  // byte offset from base of this dword
+        if (o >= skew + nbytes || o + 4 <= skew) continue;
+        const uint32_t word = *(const uint32_t*)(base + o);
 #pragma unroll
-  for (int i = 0; i < kCatQMax; ++i) mx[i] = 0.0;
-  for (int r = tid; r < nrows; r += 256) {
-    const uint8_t* cr = a.codes + (row0 + r) * F;
-    for (int f = 0; f < F; ++f) {
-      const int c = cr[f];
-      if (c > a.nlev[f])
-        atomicAdd(&cnt[kCatPMax], 1);
-      else if (c > 0)
-        atomicAdd(&cnt[a.doff[f] - doff0 + c - 1], 1);
+        for (int j = 0; j < 4; ++j) {
+          const int64_t b = o + j - skew;  // byte index in the chunk's codes
+          if (b < 0 || b >= nbytes) continue;
+          const int f = (int)(b % F);
+          const int c = (word >> (8 * j)) & 0xFF;
+          if (c > t_nlev[f])
+            ++nb;
+          else if (c > 0)
+            flag[t_doff[f] + c - 1] = 1;
+        }
+      }
     }
-    const double* xr = a.Xn + (row0 + r) * a.q;
-#pragma unroll
-    for (int i = 0; i < kCatQMax; ++i)
-      // finite values only: a NaN / Inf row fails its own partition (non-finite
-      // log-likelihood) and must not widen the shared fixed-point grid of the
-      // column for every other partition
-      if (i < a.q && isfinite(xr[i])) mx[i] = fmax(mx[i], fabs(xr[i]));
+    if (nb) atomicAdd(&nbad, nb);
   }
-  // max is order-free: wave butterfly, then the 4 waves
+
+  // ---- numeric columns: doubles [row0 q, (row0 + nrows) q) -------------------
+  if (q > 0) {
+    const double* xb = a.Xn + row0 * q;
+    const int64_t ne = (int64_t)nrows * q;
+    const int64_t wstride = 4LL * q * 64;  // doubles per workgroup iteration (a multiple of q)
+    double mx[kCatQMax];
 #pragma unroll
-  for (int i = 0; i < kCatQMax; ++i) {
+    for (int s = 0; s < kCatQMax; ++s) mx[s] = 0.0;
+    for (int64_t e0 = (int64_t)wid * q * 64; e0 < ne; e0 += wstride) {
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) mx[i] = fmax(mx[i], __shfl_xor(mx[i], o));
-    if ((tid & 63) == 0) cmax[tid >> 6][i] = mx[i];
+      for (int s = 0; s < kCatQMax; ++s) {
+        if (s < q) {
+          const int64_t e = e0 + s * 64 + lane;
+          if (e < ne) {
+            const double x = xb[e];
+            // finite values only: a NaN / Inf row fails its own partition
+            if (isfinite(x)) mx[s] = fmax(mx[s], fabs(x));
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < kCatQMax; ++s)
+      if (s < q)
+        __hip_atomic_fetch_max(&cmax[(s * 64 + lane) % q], (unsigned long long)__double_as_longlong(mx[s]),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   __syncthreads();
-  for (int d = tid; d < D; d += 256) counts[(int64_t)chunk * D + d] = cnt[d];
-  if (tid == 0) bad[chunk] = cnt[kCatPMax];
-  if (tid < a.q)
-    colmax[(int64_t)chunk * kCatQMax + tid] =
-        fmax(fmax(cmax[0][tid], cmax[1][tid]), fmax(cmax[2][tid], cmax[3][tid]));
+  for (int d = tid; d < D; d += 256) counts[(int64_t)chunk * D + d] = flag[d];
+  if (tid == 0) bad[chunk] = nbad;
+  if (tid < q) colmax[(int64_t)chunk * kCatQMax + tid] = __longlong_as_double((long long)cmax[tid]);
 }
 
 // Per partition: a selected dummy level with no rows -> the reference's

@@ -281,9 +281,10 @@ struct CatArgs {
   int32_t g_off[kCatMaxFactors];   // LDS: [rep][nlev] gradient
   int32_t pr_off[kCatMaxPairs];    // LDS: pair (f < g) [rep][nlev_f][nlev_g]
   int32_t pr_rep[kCatMaxPairs];
-  // fixed-point scales of the int64 histograms (power-of-two: [0] w and the
-  // pair cells, [1] the gradient residuals, [2 + i] w x_i of numeric column i)
-  double hscale[kCatQMax + 2];
+  // fixed-point scales of the int64 histograms per partition, device
+  // [K][kCatQMax + 2] (powers of two: [0] w and the pair cells, [1] the
+  // gradient residuals, [2 + i] w x_i of numeric column i)
+  const double* hscale;
 };
 
 // Row repartitioning (partition_rows.hip): stable counting sort by partition id.
@@ -359,6 +360,12 @@ hipError_t launch_reduce_partitions(const double* sig_inv, const double* sig_inv
                                     hipStream_t s);
 hipError_t launch_simulate(double* X, double* y, int64_t n, int p, uint64_t seed,
                            int64_t row0, hipStream_t s);
+
+// Column moments (moments.hip): out [5, p] = count, mean, M2, min, max; ws
+// holds (5 G + 5) p doubles.
+hipError_t launch_column_moments(const double* X, int64_t n, int p, double* out, double* ws,
+                                 int G, int64_t rows_per_range, hipStream_t s);
+void column_moments_plan(int64_t n, int p, int* G, int64_t* rows_per_range);
 
 void set_error(const std::string& msg);
 

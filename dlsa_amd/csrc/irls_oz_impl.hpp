@@ -151,6 +151,30 @@ constexpr int kMaxPiecesPerWave = 7;  // 1-KiB DMA pieces of a block per consume
 #ifndef DLSA_OZ_DBATCH
 #define DLSA_OZ_DBATCH 1
 #endif
+// byte offset of digit plane d in a feature's 48-byte image entry
+__host__ __device__ constexpr int plane_off(int d) { return 8 * d; }
+// producers hold 4 rows of a feature per lane (DLSA_OZ_R4 1, oz_producer_r4):
+// in-register byte transposes; 0: 8 lanes per row, DPP quad transposes
+#ifndef DLSA_OZ_R4
+#define DLSA_OZ_R4 1
+#endif
+// fold the last tile row into 5 MFMAs per tile when it holds <= 5 features
+// (DLSA_OZ_EDGE 1, OzConsumer)
+#ifndef DLSA_OZ_EDGE
+#define DLSA_OZ_EDGE 0
+#endif
+// the last DMA piece of a block as its final 1 KiB, overlapping the piece
+// before it with the same bytes (DLSA_OZ_OVL 1: whole-wave, no lane
+// predicate; 0: only the lanes inside the block; the producer schedules
+// always overlap)
+#ifndef DLSA_OZ_OVL
+#define DLSA_OZ_OVL 0
+#endif
+// DMA pieces per block and wave issued by the producers (DLSA_OZ_PDMA, with
+// the consumer schedules 0-2; see the DMA section of irls_oz_kernel)
+#ifndef DLSA_OZ_PDMA
+#define DLSA_OZ_PDMA 1
+#endif
 // per-feature magic constants instead of a per-value ldexp (DLSA_OZ_MAGICF 1)
 #ifndef DLSA_OZ_MAGICF
 #define DLSA_OZ_MAGICF 1
@@ -290,21 +314,21 @@ __device__ __forceinline__ int digit_exponent(uint32_t xhi, uint32_t zbits, doub
 // cycle stamps (s_memtime) of the iteration's phases, summed over the chunk
 // and added to g_oz_prof[slot] at its end (one vector atomic per wave).
 #ifdef DLSA_OZ_PROF
-static __device__ unsigned long long g_oz_prof[16];  // per translation unit
+static __device__ unsigned long long g_oz_prof[32];  // per translation unit: [4 wid + i]
 static inline int oz_prof_read_impl(unsigned long long* out) {
   if (hipDeviceSynchronize() != hipSuccess) return -1;
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_oz_prof), 16 * 8) != hipSuccess) return -1;
-  unsigned long long z[16] = {0};
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_oz_prof), z, 16 * 8) == hipSuccess ? 0 : -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_oz_prof), 32 * 8) != hipSuccess) return -1;
+  unsigned long long z[32] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_oz_prof), z, 32 * 8) == hipSuccess ? 0 : -1;
 }
 #define OZ_STAMP(v) const uint64_t v = __builtin_readcyclecounter()
 #define OZ_STAMP_VAR(v) uint64_t v = 0
 #define OZ_STAMP_SET(v) v = __builtin_readcyclecounter()
 #define OZ_ADD(i, d) prof[i] += (d)
-#define OZ_DECL uint64_t prof[6] = {0, 0, 0, 0, 0, 0}
+#define OZ_DECL uint64_t prof[4] = {0, 0, 0, 0}
 #define OZ_FLUSH(base)                                                        \
   if (lane == 0)                                                              \
-    for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&g_oz_prof[(base) + i_], prof[i_])
+    for (int i_ = 0; i_ < 4; ++i_) atomicAdd(&g_oz_prof[(base) + i_], prof[i_])
 #else
 #define OZ_STAMP(v)
 #define OZ_STAMP_VAR(v)
@@ -327,14 +351,39 @@ struct OzConsumer {
   static constexpr int TW = TL::TW;
   static constexpr int PMAX = 16 * NT;
   static constexpr int NB = ozk::NL > 5 ? 6 : 5;  // B quads
+  // Edge folding (DLSA_OZ_EDGE): the last tile row I = NT - 1 holds only
+  // se = P - 16 (NT - 1) features.  When se <= 5 its 16 A rows carry three
+  // groups of se rows -- group g = the digit pair (2g, 2g+1) of the se edge
+  // features -- so one MFMA against B quad b adds level 2g + b to group g:
+  // 5 MFMAs per edge tile and block (b = 0..4) instead of 9, and the store
+  // sums L_k = acc_k[e] + acc_{k-2}[se + e] + acc_{k-4}[2 se + e], the same
+  // integers the unfolded tile accumulates (bit-identical Sig_inv).
+  static constexpr bool kEdge = DLSA_OZ_EDGE && ozk::ND == 5 && ozk::NL == 5;
+  static constexpr int kEdgeTiles = [] {
+    int c = 0;
+    for (int t = 0; t < TW; ++t) c += TL::I_of(t) == NT - 1;
+    return c;
+  }();
   oz_i4 acc[TW > 0 ? TW : 1][ozk::NL];
+  bool fold = false;    // se <= 5 (wave-uniform)
+  int se = 16;          // features of the last tile row
+  int e_off = 0;        // this lane's edge A operand: byte offset of (feature, pair)
+  uint32_t m_lo = 0, m_hi = 0;  // its masks: group < 3, group < 2
 
-  __device__ __forceinline__ void init() {
+  __device__ __forceinline__ void init(int P, int lane) {
     wv_static_for<(TW > 0 ? TW : 1)>([&](auto iI) {
       constexpr int i = decltype(iI)::value;
 #pragma unroll
       for (int k = 0; k < ozk::NL; ++k) acc[i][k] = oz_i4{0, 0, 0, 0};
     });
+    se = P - 16 * (NT - 1);
+    fold = kEdge && kEdgeTiles > 0 && se <= 5;
+    if (fold) {
+      const int i = lane & 15, grp = i / se, e = i - grp * se;
+      e_off = (16 * (NT - 1) + e) * ozk::kFeatBytes + 16 * (grp < 3 ? grp : 0);
+      m_lo = grp < 3 ? 0xFFFFFFFFu : 0u;
+      m_hi = grp < 2 ? 0xFFFFFFFFu : 0u;  // group 2: (d4, 0)
+    }
   }
 
   // the image of one 32-row block whose x started at xs (LDS); tick() is
@@ -343,6 +392,11 @@ struct OzConsumer {
   // read while the MFMAs of tile t issue.
   template <typename Tick>
   __device__ __forceinline__ void consume(const char* xs, int p, int lane, Tick&& tick) {
+    consume_quads(xs, p, lane, tick);
+  }
+
+  template <typename Tick>
+  __device__ __forceinline__ void consume_quads(const char* xs, int p, int lane, Tick&& tick) {
     if constexpr (TW > 0) {
       const int i = lane & 15, g = lane >> 4;
       // lane group g: the image of producer wave g (its 8 rows of the block)
@@ -363,6 +417,14 @@ struct OzConsumer {
         A2[u] = *(const oz_i4*)(im + fa + 16);
         if constexpr (ozk::ND == 5) A4[u] = *(const u2*)(im + fa + 32);
       };
+      // the folded edge operand (one 16-byte read per block, all strips)
+      oz_i4 Ae = oz_i4{0, 0, 0, 0};
+      if constexpr (kEdge && kEdgeTiles > 0) {
+        if (fold) {
+          const oz_i4 q = *(const oz_i4*)(xs + g * ozk::RPW * p * 8 + e_off);
+          Ae = oz_i4{(int)(q.x & m_lo), (int)(q.y & m_lo), (int)(q.z & m_hi), (int)(q.w & m_hi)};
+        }
+      }
       loadB(std::integral_constant<int, TL::J_of(0)>{}, 0);
       loadA(std::integral_constant<int, 0>{}, 0);
       wv_static_for<TW>([&](auto tI) {
@@ -370,10 +432,15 @@ struct OzConsumer {
         constexpr int J = TL::J_of(t);
         constexpr int ua = t & 1;
         constexpr int ub = TL::strip_ordinal(J) & 1;
+        constexpr bool edge = kEdge && TL::I_of(t) == NT - 1;
         if constexpr (t + 1 < TW) {
           constexpr int Jn = TL::J_of(t + 1);
           if constexpr (Jn != J) loadB(std::integral_constant<int, Jn>{}, ub ^ 1);
-          loadA(std::integral_constant<int, t + 1>{}, ua ^ 1);
+          if constexpr (kEdge && TL::I_of(t + 1) == NT - 1) {
+            if (!fold) loadA(std::integral_constant<int, t + 1>{}, ua ^ 1);
+          } else {
+            loadA(std::integral_constant<int, t + 1>{}, ua ^ 1);
+          }
         }
         __builtin_amdgcn_sched_barrier(0);
         // B quad b: bytes 0-7 digit b, bytes 8-15 digit b - 1 (zero for b = 0)
@@ -384,6 +451,16 @@ struct OzConsumer {
         for (int b = 1; b < ozk::ND; ++b)
           Bq[b] = oz_i4{(int)d[b].x, (int)d[b].y, (int)d[b - 1].x, (int)d[b - 1].y};
         if constexpr (NB > 5) Bq[5] = oz_i4{0, 0, (int)d[4].x, (int)d[4].y};
+        if constexpr (edge) {
+          if (fold) {  // wave-uniform
+#pragma unroll
+            for (int b = 0; b < 5; ++b)
+              acc[t][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Ae, Bq[b], acc[t][b], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            tick(std::integral_constant<int, t>{});
+            return;
+          }
+        }
         const oz_i4 a0 = A0[ua], a2 = A2[ua];
         if constexpr (ozk::ND == 4) {  // levels 0-4: 8 MFMAs (level 4: (1,3) (2,2) (3,1))
           const oz_i4 b4 = oz_i4{0, 0, (int)d[3].x, (int)d[3].y};
@@ -432,14 +509,48 @@ struct OzConsumer {
     }
   }
 
-  // H tiles into the chunk's slab (newton_solve.hip layout), scaled back
-  __device__ __forceinline__ void store(double* sH, const int* ex, int lane) {
+  // H tiles into the chunk's slab (newton_solve.hip layout), scaled back.
+  // scratch: this wave's LDS for the folded edge tiles (5 x 16 x 16 int32 each)
+  __device__ __forceinline__ void store(double* sH, const int* ex, int lane, int* scratch) {
     if constexpr (TW > 0) {
       const int fl = lane & 15, q = lane >> 4;
       wv_static_for<TW>([&](auto iI) {
         constexpr int t = decltype(iI)::value;
         constexpr int I = TL::I_of(t), J = TL::J_of(t);
         constexpr int ts = I * (I + 1) / 2 + J;
+        if constexpr (kEdge && I == NT - 1) {
+          if (fold) {
+            // acc[t][b] at C row R = 4 q + r, col fl -> S[b][R][fl]
+#pragma unroll
+            for (int b = 0; b < 5; ++b)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) scratch[(b * 16 + 4 * q + r) * 16 + fl] = acc[t][b][r];
+            const int ej = ex[16 * J + fl];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int row = 4 * q + r;
+              double v = 0.0;  // rows past the last feature (f >= P): never read
+              if (row < se) {
+                oz_i4 L[1][5];
+                int lv[5];
+#pragma unroll
+                for (int k = 0; k < 5; ++k) {
+                  int x = scratch[(k * 16 + row) * 16 + fl];
+                  if (k >= 2) x += scratch[((k - 2) * 16 + se + row) * 16 + fl];
+                  if (k >= 4) x += scratch[((k - 4) * 16 + 2 * se + row) * 16 + fl];
+                  lv[k] = x;
+                }
+#pragma unroll
+                for (int k = 0; k < 5; ++k) L[0][k] = oz_i4{lv[k], 0, 0, 0};
+                v = __builtin_amdgcn_ldexp(ozk::level_value(L[0], 0),
+                                           ej + ex[16 * I + row] - 12);
+              }
+              sH[ts * 256 + row * 16 + fl] = v;
+            }
+            scratch += 5 * 256;
+            return;
+          }
+        }
         const int ej = ex[16 * J + fl];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {  // i32 16x16 C/D map: row 4 (l >> 4) + r, col l & 15
@@ -451,6 +562,242 @@ struct OzConsumer {
     }
   }
 };
+
+// ---- producer waves, row quads in lanes (DLSA_OZ_R4) ------------------------
+// Lane (q, s) = (lane >> 4, lane & 15) holds 4 rows of features 16 k + s,
+// k = 0 .. NT-1: rows 4 (q & 1) .. 4 (q & 1) + 3 of this wave's 8 rows of
+// block 2m + (q >> 1).  With the 4 rows of a feature in one lane, a digit
+// plane of 4 rows is a byte transpose of the lane's own words (8 v_perm for
+// the four low-dword planes, 3 for the top digit) instead of DPP quad
+// exchanges across lanes (4 VALU per word), the x reads of a wave row are 16
+// consecutive doubles (no bank conflicts), and theta, the gradient partials
+// and the digit constants take NT registers pairs per lane instead of 2 NT.
+// eta of the 4 rows: 4 FMA chains over the lane's NT features, then a
+// reduce-scatter over the 16 lanes of the feature slots (DPP row_ror:8,
+// row_half_mirror, 2 quad_perm) leaves lane s with row s >> 2; one
+// transcendental chain for the 16 rows of the wave (4 replicas per row);
+// row_newbcast brings each row's sqrt(w) and residual back to the 16 lanes.
+// Same image layout, ownership rule and epilogue as the quad-transpose
+// producers below.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+template <int NT, bool STD, int FAM, typename SlotX, typename Dma>
+__device__ __forceinline__ void oz_producer_r4(const PassArgs& a, char* smem, int wid, int lane,
+                                               int tid, int nb, int nit, int sbytes,
+                                               int xs_bytes, SlotX&& slot_x, const double* bet,
+                                               const double* stdv, const int* ex, int chunk,
+                                               Dma&& issue_pair) {
+  using namespace ozk;
+  static_assert(ND == 5 && DLSA_OZ_MAGICF, "row-quad producers: 5 digits, magic constants");
+  constexpr int PMAX = 16 * NT;
+  const int p = a.p, P = a.P, ic = a.intercept;
+  const int nrows = __builtin_amdgcn_readfirstlane(a.chunk_rows[blockIdx.x]);
+  const int pw = wid;
+  const int q = lane >> 4, s = lane & 15;
+  const int Xq = q >> 1, hq = q & 1;
+  const int rbase = pw * RPW + 4 * hq;  // block row of this lane's row 0
+  const bool up8 = s >= 8, up4 = ((s >> 2) & 1) != 0;
+  const int myrow = s >> 2;             // the row whose eta this lane ends with
+  double beta[NT], gacc[NT], mg[NT];
+#pragma unroll
+  for (int k = 0; k < NT; ++k) {
+    const int f = 16 * k + s;
+    beta[k] = bet[f];
+    mg[k] = __builtin_amdgcn_ldexp(MAGIC, ex[f] - GBITS);
+    gacc[k] = 0.0;
+  }
+  const bool fin_last = 16 * (NT - 1) + s < P;  // the last tile's feature is < P
+  double llacc = 0.0, lprod = 1.0;
+
+  // producer-issued DMA (DLSA_OZ_SCHED 3: right after the barrier, 4: after
+  // the row phase, 5: after the digits); each wave waits for its own pieces
+  // before the next barrier, which then publishes all of them
+  // (DLSA_OZ_PDMA > 0 with a consumer schedule: the producers' share of the
+  // pieces, at the iteration start as in 3)
+  constexpr int kSched = DLSA_OZ_SCHED >= 3 ? DLSA_OZ_SCHED : (DLSA_OZ_PDMA > 0 ? 3 : 0);
+  if constexpr (kSched >= 3) {
+    issue_pair(-1);
+    wv_wait_vmcnt<0>();
+  }
+  OZ_DECL;
+  for (int m = 0; m < nit; ++m) {
+    OZ_STAMP(t0);
+    if constexpr (kSched >= 3) wv_wait_vmcnt<0>();
+    barrier();  // B_m
+    OZ_STAMP(t1);
+    OZ_ADD(0, t1 - t0);
+    if constexpr (kSched == 3) issue_pair(m);
+    if (2 * m >= nb || (DLSA_OZ_ABLATE & 1)) {  // the last iteration only consumes
+      if constexpr (kSched >= 4) issue_pair(m);
+      continue;
+    }
+    const int b = 2 * m + Xq;
+    char* xq = slot_x(b);
+    const double* yq = (const double*)(smem + (b % NSLOT) * sbytes + 16 + xs_bytes);
+    const int leftq = nrows - b * RB;
+    // workgroup-uniform: both blocks full
+    const bool full = nrows - 2 * m * RB >= 2 * RB;
+    double v[4][NT], e[4];
+    auto row_phase = [&](auto maskI) {
+      constexpr bool MASK = decltype(maskI)::value;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rowB = rbase + r;
+        const bool valid = rowB < leftq;
+        const double* xr = (const double*)xq + rowB * p + (s - ic);
+        double er = 0.0;
+#pragma unroll
+        for (int k = 0; k < NT; ++k) {
+          const int f = 16 * k + s;
+          double x = xr[16 * k];
+          if constexpr (DLSA_OZ_CHECK) {  // ownership rule: own rows for f < P
+            const int el = rowB * p + f - ic;
+            if (f >= ic && f < P && (el < pw * RPW * p || el >= (pw + 1) * RPW * p))
+              x = __builtin_nan("");
+          }
+          if constexpr (STD) x = (x - stdv[f]) * stdv[PMAX + f];
+          if (k == 0 && ic && s == 0) x = 1.0;
+          const bool fin = k < NT - 1 || fin_last;  // padding features f >= P: 0
+          if constexpr (MASK)
+            x = (valid && fin) ? x : 0.0;
+          else
+            x = fin ? x : 0.0;
+          v[r][k] = x;
+          er = fma(x, beta[k], er);
+        }
+        e[r] = er;
+      }
+    };
+    if (full)
+      row_phase(std::false_type{});
+    else
+      row_phase(std::true_type{});
+    // reduce-scatter of the 4 row sums over the 16 feature slots
+    double e01, e23;
+    {
+      const double s0 = up8 ? e[0] : e[2], s1 = up8 ? e[1] : e[3];  // the partner's rows
+      const double k0 = up8 ? e[2] : e[0], k1 = up8 ? e[3] : e[1];  // kept
+      e01 = k0 + dpp_f64<0x128>(s0);  // row_ror:8 = lane s ^ 8
+      e23 = k1 + dpp_f64<0x128>(s1);
+    }
+    double eh;
+    {
+      const double sn = up4 ? e01 : e23, kp = up4 ? e23 : e01;
+      eh = kp + dpp_f64<0x141>(sn);  // row_half_mirror: bit 2 of s flipped
+    }
+    eh += dpp_f64<0xB1>(eh);  // quad_perm [1,0,3,2]
+    eh += dpp_f64<0x4E>(eh);  // quad_perm [2,3,0,1]
+    // one transcendental chain for the wave's 16 rows (row rbase + myrow)
+    double swh, rh;
+    {
+      const bool valid = rbase + myrow < leftq;
+      const double yv = valid ? yq[rbase + myrow] : 0.0;
+      if constexpr (FAM == FAMILY_LOGISTIC) {
+        const double eqv = exp(-0.5 * fabs(eh));
+        const double ea = eqv * eqv;
+        const double inv = wv_rcp(1.0 + ea);
+        const double mu = eh >= 0.0 ? inv : ea * inv;
+        swh = eqv * inv;
+        rh = yv - mu;
+        if (valid && (s & 3) == 0) {
+          llacc += yv * eh - fmax(eh, 0.0);
+          lprod *= 1.0 + ea;
+        }
+      } else {  // gaussian (OLS): mu = eta, w = 1, ll = -rss / 2
+        swh = 1.0;
+        rh = yv - eh;
+        if (valid && (s & 3) == 0) llacc -= 0.5 * rh * rh;
+      }
+      if (!valid) {
+        swh = 0.0;
+        rh = 0.0;
+      }
+    }
+    double sw[4], res[4];
+    sw[0] = dpp_f64<0x150>(swh);  // row_newbcast:4r -- row r's values to the 16 lanes
+    sw[1] = dpp_f64<0x154>(swh);
+    sw[2] = dpp_f64<0x158>(swh);
+    sw[3] = dpp_f64<0x15C>(swh);
+    res[0] = dpp_f64<0x150>(rh);
+    res[1] = dpp_f64<0x154>(rh);
+    res[2] = dpp_f64<0x158>(rh);
+    res[3] = dpp_f64<0x15C>(rh);
+    if constexpr (kSched == 4) issue_pair(m);
+    OZ_STAMP(t2);
+    OZ_ADD(1, t2 - t1);
+    // ---- gradient and the digit image of the 4 rows ---------------------------
+    char* img = xq + pw * RPW * p * 8 + 4 * hq;
+#pragma unroll
+    for (int k = 0; k < NT; ++k) {
+      gacc[k] = fma(v[0][k], res[0], gacc[k]);
+      gacc[k] = fma(v[1][k], res[1], gacc[k]);
+      gacc[k] = fma(v[2][k], res[2], gacc[k]);
+      gacc[k] = fma(v[3][k], res[3], gacc[k]);
+      uint32_t lo[4], hi[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const double t = fma(v[r][k], sw[r], mg[k]);
+        lo[r] = __double2loint(t);
+        hi[r] = __double2hiint(t);
+      }
+      // byte j of lo = digit 4 - j; byte 0 of hi = digit 0 (row order = byte order)
+      const uint32_t u01 = perm(lo[1], lo[0], 0x05010400u), w01 = perm(lo[1], lo[0], 0x07030602u);
+      const uint32_t u23 = perm(lo[3], lo[2], 0x05010400u), w23 = perm(lo[3], lo[2], 0x07030602u);
+      const uint32_t d4 = perm(u23, u01, 0x05040100u) ^ 0x80808080u;
+      const uint32_t d3 = perm(u23, u01, 0x07060302u) ^ 0x80808080u;
+      const uint32_t d2 = perm(w23, w01, 0x05040100u) ^ 0x80808080u;
+      const uint32_t d1 = perm(w23, w01, 0x07060302u) ^ 0x80808080u;
+      const uint32_t d0 = perm(perm(hi[3], hi[2], 0x05010400u), perm(hi[1], hi[0], 0x05010400u),
+                               0x05040100u) ^ 0x80808080u;
+      char* fe = img + (16 * k + s) * kFeatBytes;
+      *(uint32_t*)(fe + plane_off(0)) = d0;
+      *(uint32_t*)(fe + plane_off(1)) = d1;
+      *(uint32_t*)(fe + plane_off(2)) = d2;
+      *(uint32_t*)(fe + plane_off(3)) = d3;
+      *(uint32_t*)(fe + plane_off(4)) = d4;
+    }
+    if constexpr (kSched == 5) issue_pair(m);
+#ifdef DLSA_OZ_PROF
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+    OZ_STAMP(t3);
+    OZ_ADD(2, t3 - t2);
+  }
+  OZ_FLUSH(4 * pw);
+  __syncthreads();  // S1 (the consumers' S1): the ring is free
+
+  // ---- epilogue: gradient and log-likelihood partials --------------------------
+  double* red = (double*)smem;  // the ring: [NPW][PMAX + 1]
+#pragma unroll
+  for (int k = 0; k < NT; ++k) {
+    double g = gacc[k];
+    g += __shfl_xor(g, 16);
+    g += __shfl_xor(g, 32);
+    if (q == 0) red[pw * (PMAX + 1) + 16 * k + s] = g;
+  }
+  if constexpr (FAM == FAMILY_LOGISTIC) llacc -= log(lprod);
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) llacc += __shfl_xor(llacc, o);
+  if (lane == 0) red[pw * (PMAX + 1) + PMAX] = llacc;
+  __syncthreads();  // S2
+  for (int f = tid; f < PMAX; f += 64 * NPW) {
+    double sg = 0.0;
+#pragma unroll
+    for (int w = 0; w < NPW; ++w) sg += red[w * (PMAX + 1) + f];
+    a.slab_g[(int64_t)chunk * PMAX + f] = sg;
+  }
+  if (tid == 0) {
+    double sg = 0.0;
+#pragma unroll
+    for (int w = 0; w < NPW; ++w) sg += red[w * (PMAX + 1) + PMAX];
+    a.slab_ll[chunk] = sg;
+  }
+}
 
 template <int NT, bool STD, int FAM>
 __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(const PassArgs a) {
@@ -531,56 +878,95 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
     return smem + (blk % NSLOT) * sbytes + 16 + (start & 15);
   };
 
+  // ---- LDS-DMA of the X / y blocks --------------------------------------------
+  // Issued by the consumer waves (DLSA_OZ_SCHED 0-2) or by the producer waves
+  // (3-5); dw = the issuing wave's index among its four.  Wave dw's pieces of
+  // a block: X pieces dw, dw + 4, ... and (dw = 3) the block's y.  Scalar
+  // bases per block; piece i (a compile-time index) is two scalar adds and the
+  // DMA.  The last piece either runs with only the lanes inside the block
+  // (consumer schedules) or is the block's final 1 KiB, overlapping the piece
+  // before it with the same bytes (producer schedules: whole-wave, no lane
+  // predicate -- the predicated form fails instruction selection in hipcc 7.2
+  // in the producers' scope).
+  constexpr bool kProdDma = DLSA_OZ_SCHED >= 3;
+  static_assert(!kProdDma || DLSA_OZ_R4, "producer-issued DMA: row-quad producers");
+  // DLSA_OZ_PDMA = KP > 0 with a consumer schedule: the producers issue each
+  // block's pieces i < KP (their own DMA share) at the iteration start, the
+  // consumers the rest -- the DMA issue cost split between the two wave types
+  constexpr int KP = kProdDma ? kMaxPiecesPerWave : DLSA_OZ_PDMA;
+  static_assert(KP == 0 || DLSA_OZ_R4, "producer-issued DMA: row-quad producers");
+  constexpr bool kOvl = kProdDma || DLSA_OZ_OVL || KP > 0;
+  const int dw = wid >= NPW ? wid - NPW : wid;
+  const uintptr_t xcb = (uintptr_t)(a.X + row0 * p) & ~(uintptr_t)15;
+  const __amdgpu_buffer_rsrc_t xr = wv_rsrc(xcb, a.x_last16 + 16 - xcb);
+  const uintptr_t ycb = (uintptr_t)(a.y + row0);
+  const __amdgpu_buffer_rsrc_t yr = wv_rsrc(ycb, a.y_last4 + 4 - ycb);
+  const int npw = (np - dw + NCW - 1) / NCW;
+  const int last_rem = xs_bytes - (np - 1) * 1024;  // bytes of the last piece
+  // a block's slot LDS offset and the buffer offset of its 16-B-aligned start
+  auto blk_lds = [&](int blk) { return __builtin_amdgcn_readfirstlane((blk % NSLOT) * sbytes); };
+  auto blk_soff = [&](int blk) {
+    const uintptr_t start = (uintptr_t)(a.X + (row0 + (int64_t)blk * RB) * p);
+    return __builtin_amdgcn_readfirstlane((int)((start & ~(uintptr_t)15) - xcb));
+  };
+  auto issue_x = [&](auto iI, int lds, int soff) {
+    constexpr int i = decltype(iI)::value;
+    if (i < npw) {  // uniform
+      const int j = dw + NCW * i;
+      if constexpr (kOvl) {
+        const int off = j == np - 1 ? xs_bytes - 1024 : j * 1024;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (wlds_void_t*)(smem + lds + 16 + off), 16,
+                                                 lane * 16, soff + off, 0, DLSA_OZ_DMA_AUX);
+      } else if (j != np - 1 || lane * 16 < last_rem) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (wlds_void_t*)(smem + lds + 16 + j * 1024),
+                                                 16, lane * 16, soff + j * 1024, 0,
+                                                 DLSA_OZ_DMA_AUX);
+      }
+    }
+  };
+  auto issue_y = [&](int blk, int lds) {
+    if (dw == NCW - 1)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(yr, (wlds_void_t*)(smem + lds + 16 + xs_bytes), 4,
+                                               lane * 4, blk * RB * 8, 0, 0);
+  };
+  // all of a block's pieces from piece I0 on
+  auto issue_rest = [&](auto I0, int blk, int lds, int soff) {
+    wv_static_for<kMaxPiecesPerWave>([&](auto iI) {
+      if constexpr (decltype(iI)::value >= decltype(I0)::value) issue_x(iI, lds, soff);
+    });
+    issue_y(blk, lds);
+  };
+  // producer schedules: blocks 2m+2, 2m+3 (into the slots of 2m-4, 2m-3, free
+  // since B_m), or blocks 0, 1 before the loop (m = -1)
+  // (all pieces + y with kProdDma, else the pieces i < KP)
+  auto issue_pair = [&](int m) {
+#pragma unroll
+    for (int X = 2; X < 4; ++X) {
+      const int blk = 2 * m + X;
+      if (blk < nb) {
+        const int lds = blk_lds(blk), soff = blk_soff(blk);
+        wv_static_for<kMaxPiecesPerWave>([&](auto iI) {
+          if constexpr (decltype(iI)::value < KP) issue_x(iI, lds, soff);
+        });
+        if constexpr (kProdDma) issue_y(blk, lds);
+      }
+    }
+  };
+
   if (wid >= NPW) {
     // ======================= consumer waves ==================================
     const int cw = wid - NPW;
-    const uintptr_t xcb = (uintptr_t)(a.X + row0 * p) & ~(uintptr_t)15;
-    const __amdgpu_buffer_rsrc_t xr = wv_rsrc(xcb, a.x_last16 + 16 - xcb);
-    const uintptr_t ycb = (uintptr_t)(a.y + row0);
-    const __amdgpu_buffer_rsrc_t yr = wv_rsrc(ycb, a.y_last4 + 4 - ycb);
-    // this wave's DMA pieces of a block: X pieces cw, cw + 4, ... (the last one
-    // only over its lanes inside the block), and (cw = 3) the block's y.
-    // Scalar bases per block; piece i (a compile-time index) is two scalar
-    // adds and the DMA.
-    const int npw = (np - cw + NCW - 1) / NCW;
-    const int last_rem = xs_bytes - (np - 1) * 1024;  // bytes of the last piece
-    // a block's slot LDS offset and the buffer offset of its 16-B-aligned start
-    auto blk_lds = [&](int blk) { return __builtin_amdgcn_readfirstlane((blk % NSLOT) * sbytes); };
-    auto blk_soff = [&](int blk) {
-      const uintptr_t start = (uintptr_t)(a.X + (row0 + (int64_t)blk * RB) * p);
-      return __builtin_amdgcn_readfirstlane((int)((start & ~(uintptr_t)15) - xcb));
-    };
-    auto issue_x = [&](auto iI, int lds, int soff) {
-      constexpr int i = decltype(iI)::value;
-      if (i < npw) {  // uniform
-        const int j = cw + NCW * i;
-        if (j != np - 1 || lane * 16 < last_rem)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (wlds_void_t*)(smem + lds + 16 + j * 1024),
-                                                   16, lane * 16, soff + j * 1024, 0,
-                                                   DLSA_OZ_DMA_AUX);
-      }
-    };
-    auto issue_y = [&](int blk, int lds) {
-      if (cw == NCW - 1)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(yr, (wlds_void_t*)(smem + lds + 16 + xs_bytes), 4,
-                                                 lane * 4, blk * RB * 8, 0, 0);
-    };
-    // all of a block's pieces from piece I0 on
-    auto issue_rest = [&](auto I0, int blk, int lds, int soff) {
-      wv_static_for<kMaxPiecesPerWave>([&](auto iI) {
-        if constexpr (decltype(iI)::value >= decltype(I0)::value) issue_x(iI, lds, soff);
-      });
-      issue_y(blk, lds);
-    };
     auto run = [&](auto cwI) {
       constexpr int CW = decltype(cwI)::value;
       constexpr int TW = OzConsumer<NT, CW>::TW;
       if constexpr (DLSA_OZ_PRIO > 0) __builtin_amdgcn_s_setprio(DLSA_OZ_PRIO);
       OzConsumer<NT, CW> C;
-      C.init();
-      for (int b = 0; b < 2 && b < nb; ++b)
-        issue_rest(std::integral_constant<int, 0>{}, b, blk_lds(b), blk_soff(b));
-      wv_wait_vmcnt<0>();
+      C.init(P, lane);
+      if constexpr (!kProdDma) {
+        for (int b = 0; b < 2 && b < nb; ++b)
+          issue_rest(std::integral_constant<int, KP>{}, b, blk_lds(b), blk_soff(b));
+        wv_wait_vmcnt<0>();
+      }
       OZ_DECL;
       for (int m = 0; m < nit; ++m) {
         OZ_STAMP(t0);
@@ -601,7 +987,12 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
         const bool c0 = m >= 1 && !(DLSA_OZ_ABLATE & 2);
         const bool c1 = c0 && 2 * m - 1 < nb;
         OZ_STAMP_VAR(t2);
-        if constexpr (DLSA_OZ_SCHED == 0) {
+        if constexpr (kProdDma) {  // the producers issue the DMA
+          auto tickN = [&](auto) {};
+          if (c0) C.consume(slot_x(2 * m - 2), p, lane, tickN);
+          if (c1) C.consume(slot_x(2 * m - 1), p, lane, tickN);
+          OZ_STAMP_SET(t2);
+        } else if constexpr (DLSA_OZ_SCHED == 0) {
           if (c0) C.consume(slot_x(2 * m - 2), p, lane, tick0);
           if (c1) C.consume(slot_x(2 * m - 1), p, lane, tick1);
           OZ_STAMP_SET(t2);
@@ -623,21 +1014,23 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
           // of each per tile; SCHED 2: block 2m+2 at once, then a piece of
           // 2m+3 per tile), so the last pieces land while the second image's
           // MFMAs run instead of in front of the iteration's final wait
+          // (pieces i < KP: the producers')
           auto tickA = [&](auto tI) {
-            if (DLSA_OZ_SCHED == 1 && d0) issue_x(tI, l0, s0);
-            if (d1) issue_x(tI, l1, s1);
+            constexpr int i = KP + decltype(tI)::value;
+            if (DLSA_OZ_SCHED == 1 && d0) issue_x(std::integral_constant<int, i>{}, l0, s0);
+            if (d1) issue_x(std::integral_constant<int, i>{}, l1, s1);
           };
           auto tickN = [&](auto) {};
-          if (DLSA_OZ_SCHED == 2 && d0) issue_rest(std::integral_constant<int, 0>{}, 2 * m + 2, l0, s0);
+          if (DLSA_OZ_SCHED == 2 && d0) issue_rest(std::integral_constant<int, KP>{}, 2 * m + 2, l0, s0);
           if (c0) C.consume(slot_x(2 * m - 2), p, lane, tickA);
           if (c0) {
             if (DLSA_OZ_SCHED == 1 && d0)
-              issue_rest(std::integral_constant<int, TW>{}, 2 * m + 2, l0, s0);
-            if (d1) issue_rest(std::integral_constant<int, TW>{}, 2 * m + 3, l1, s1);
+              issue_rest(std::integral_constant<int, KP + TW>{}, 2 * m + 2, l0, s0);
+            if (d1) issue_rest(std::integral_constant<int, KP + TW>{}, 2 * m + 3, l1, s1);
           } else {
             if (DLSA_OZ_SCHED == 1 && d0)
-              issue_rest(std::integral_constant<int, 0>{}, 2 * m + 2, l0, s0);
-            if (d1) issue_rest(std::integral_constant<int, 0>{}, 2 * m + 3, l1, s1);
+              issue_rest(std::integral_constant<int, KP>{}, 2 * m + 2, l0, s0);
+            if (d1) issue_rest(std::integral_constant<int, KP>{}, 2 * m + 3, l1, s1);
           }
           if (c1) C.consume(slot_x(2 * m - 1), p, lane, tickN);
           OZ_STAMP_SET(t2);
@@ -650,9 +1043,11 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
         OZ_ADD(2, t2 - t1);
         OZ_ADD(3, t4 - t3);
       }
-      if (CW == 0) OZ_FLUSH(8);
+      OZ_FLUSH(4 * (NPW + CW));
       __syncthreads();  // S1
-      C.store(a.slab_H + (int64_t)chunk * (NT * (NT + 1) / 2) * 256, ex, lane);
+      // edge scratch: past the producers' reduction area at the ring's start
+      C.store(a.slab_H + (int64_t)chunk * (NT * (NT + 1) / 2) * 256, ex, lane,
+              (int*)(smem + 8192 + cw * 2 * 5 * 256 * 4));
       __syncthreads();  // S2 (the producers' reduction)
     };
     switch (cw) {
@@ -664,6 +1059,11 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
     return;
   }
 
+#if DLSA_OZ_R4
+  oz_producer_r4<NT, STD, FAM>(a, smem, wid, lane, tid, nb, nit, sbytes, xs_bytes, slot_x, bet,
+                               stdv, ex, chunk, issue_pair);
+  return;
+#endif
   // ========================= producer waves ==================================
   const int pw = wid;
   const int sl = lane / RPW;             // row phase: feature group
@@ -844,11 +1244,12 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
       for (int i = 0; i < M + NG; ++i) w[i] = perm(dpp<0x4E>(w[i]), w[i], sel2) ^ 0x80808080u;
 #pragma unroll
       for (int m2 = 0; m2 < M; ++m2)
-        *(uint32_t*)(img + (sl + LPR * m2) * kFeatBytes + (ND - 1 - jq) * 8) = w[m2];
+        *(uint32_t*)(img + (sl + LPR * m2) * kFeatBytes + plane_off(ND - 1 - jq)) = w[m2];
 #pragma unroll
       for (int g = 0; g < NG; ++g) {
         const int m0 = 4 * g, n = M - m0 < 4 ? M - m0 : 4;
-        if (jq < n) *(uint32_t*)(img + (sl + LPR * (m0 + jq)) * kFeatBytes) = w[M + g];
+        if (jq < n)
+          *(uint32_t*)(img + (sl + LPR * (m0 + jq)) * kFeatBytes + plane_off(0)) = w[M + g];
       }
     }
 #else
@@ -864,7 +1265,7 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
         const uint32_t lo = __double2loint(t);
         // lane jq: byte jq of the quad's 4 rows = digit ND - 1 - jq
         const uint32_t dq = quad_transpose(lo, sel1, sel2) ^ 0x80808080u;
-        *(uint32_t*)(img + (sl + LPR * m2) * kFeatBytes + (ND - 1 - jq) * 8) = dq;
+        *(uint32_t*)(img + (sl + LPR * m2) * kFeatBytes + plane_off(ND - 1 - jq)) = dq;
         if constexpr (ND == 4) continue;  // the low dword held all four digits
         top[m2 & 3] = __double2hiint(t);
         if ((m2 & 3) == 3 || m2 == M - 1) {  // digit 0 of up to 4 features
@@ -874,7 +1275,7 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
           const uint32_t t01 = perm(top[1], top[0], 0x05010400u);
           const uint32_t t23 = perm(top[3], top[2], 0x05010400u);
           const uint32_t tq = quad_transpose(perm(t23, t01, 0x05040100u), sel1, sel2) ^ 0x80808080u;
-          if (jq < n) *(uint32_t*)(img + (sl + LPR * (m0 + jq)) * kFeatBytes) = tq;
+          if (jq < n) *(uint32_t*)(img + (sl + LPR * (m0 + jq)) * kFeatBytes + plane_off(0)) = tq;
         }
       }
     }
@@ -885,7 +1286,7 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
     OZ_STAMP(t3);
     OZ_ADD(2, t3 - t2);
   }
-  if (pw == 0) OZ_FLUSH(0);
+  OZ_FLUSH(4 * pw);
   __syncthreads();  // S1 (the consumers' S1): the ring is free
 
   // ---- epilogue: gradient and log-likelihood partials --------------------------

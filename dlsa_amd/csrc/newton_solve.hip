@@ -23,6 +23,15 @@
 #ifndef DLSA_SOLVE_PROFILE
 #define DLSA_SOLVE_PROFILE 0
 #endif
+// Blocked triangular solves (DLSA_SOLVE_BLOCKED 1): the Cholesky keeps the
+// inverse of each 16x16 diagonal block in place of the block, the panel
+// below is A_ib Linv_bb^T (16 independent dot products per row instead of a
+// 16-step substitution) and both triangular solves run a block at a time
+// (16 lanes apply Linv_bb, every thread updates its rows) -- 2 NT barrier
+// steps instead of 2 P dependent ones.  0: the per-column solves.
+#ifndef DLSA_SOLVE_BLOCKED
+#define DLSA_SOLVE_BLOCKED 0
+#endif
 #if DLSA_SOLVE_PROFILE
 #define SOLVE_MARK(i) \
   if (k == 0 && tid == 0) tmark[i] = clock64();
@@ -205,6 +214,7 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
 #pragma unroll
       for (int j = 0; j < 16; ++j) av[j] = (act && j <= i) ? H[tri(c0 + i, c0 + j)] : 0.0;
       bool good = true;
+      double ild = 0.0;  // lane kk: 1 / L_kk
 #pragma unroll
       for (int kk = 0; kk < 16; ++kk) {
         if (kk < nb) {  // wave-uniform
@@ -212,6 +222,7 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
           good = good && dkk > 0.0 && isfinite(dkk);
           const double lkk = sqrt(dkk);
           const double il = 1.0 / lkk;
+          if (lane == kk) ild = il;
           av[kk] = (i > kk) ? av[kk] * il : (i == kk ? lkk : av[kk]);
 #pragma unroll
           for (int j = kk + 1; j < 16; ++j) {
@@ -221,9 +232,31 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
           if (lane == 0) invd[c0 + kk] = il;
         }
       }
+#if DLSA_SOLVE_BLOCKED
+      // Linv = L_bb^-1, lower: lane j (< nb) solves column j, L_bb entries
+      // broadcast from their rows' lanes; stored over L_bb
+      {
+        const int j = lane;
+        double x[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          x[r] = 0.0;
+          if (r < nb) {  // wave-uniform
+            double acc = (r == j) ? 1.0 : 0.0;
+#pragma unroll
+            for (int k = 0; k < r; ++k) acc = fma(-readlane_f64(av[k], r), x[k], acc);
+            x[r] = acc * readlane_f64(ild, r);
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (j < nb && r >= j && r < nb) H[tri(c0 + r, c0 + j)] = x[r];
+      }
+#else
 #pragma unroll
       for (int j = 0; j < 16; ++j)
         if (act && j <= i) H[tri(c0 + i, c0 + j)] = av[j];
+#endif
       if (lane == 0 && !good) red[5] = 1.0;
     }
     __syncthreads();
@@ -238,6 +271,19 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
         double x[16];
 #pragma unroll
         for (int kk = 0; kk < 16; ++kk) x[kk] = hr[kk];
+#if DLSA_SOLVE_BLOCKED
+        // L_ib = A_ib Linv_bb^T: 16 independent dot products
+        double o[16];
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+          double acc = 0.0;
+#pragma unroll
+          for (int kk = 0; kk <= m; ++kk) acc = fma(x[kk], H[tri(c0 + m, c0 + kk)], acc);
+          o[m] = acc;
+        }
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) hr[kk] = o[kk];
+#else
 #pragma unroll
         for (int kk = 0; kk < 16; ++kk) {
           x[kk] *= invd[c0 + kk];
@@ -246,6 +292,7 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
         }
 #pragma unroll
         for (int kk = 0; kk < 16; ++kk) hr[kk] = x[kk];
+#endif
       }
       __syncthreads();
       const int m = NT - b - 1;  // tile rows below the panel
@@ -302,6 +349,56 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
   }
 
   SOLVE_MARK(3)
+#if DLSA_SOLVE_BLOCKED
+  // 5. triangular solves L z = g, L^T d = z a 16-block at a time (the
+  //    diagonal blocks hold Linv_bb): 16 lanes of wave 0 apply Linv_bb (or
+  //    its transpose) to the block's right-hand side, then every thread
+  //    updates the remaining entries with the block's off-diagonal L
+  for (int f = tid; f < PP; f += 256) z[f] = f < P ? g[f] : 0.0;
+  __syncthreads();
+  for (int b = 0; b < NT; ++b) {
+    const int c0 = 16 * b;
+    if (c0 >= P) break;
+    const int nb = min(16, P - c0);
+    if (wid == 0) {
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (k < nb && k <= lane) acc = fma(H[tri(c0 + lane, c0 + k)], z[c0 + k], acc);
+      if (lane < nb) z[c0 + lane] = acc;
+    }
+    __syncthreads();
+    for (int j = c0 + 16 + tid; j < P; j += 256) {
+      double acc = z[j];
+      const double* lr = H + tri(j, c0);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) acc = fma(-lr[k], z[c0 + k], acc);
+      z[j] = acc;
+    }
+    __syncthreads();
+  }
+  for (int b = NT - 1; b >= 0; --b) {
+    const int c0 = 16 * b;
+    if (c0 >= P) continue;
+    const int nb = min(16, P - c0);
+    if (wid == 0) {
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (k < nb && k >= lane) acc = fma(H[tri(c0 + k, c0 + lane)], z[c0 + k], acc);
+      if (lane < nb) z[c0 + lane] = acc;
+    }
+    __syncthreads();
+    for (int j = tid; j < c0; j += 256) {
+      double acc = z[j];
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (k < nb) acc = fma(-H[tri(c0 + k, j)], z[c0 + k], acc);
+      z[j] = acc;
+    }
+    __syncthreads();
+  }
+#else
   // 5. triangular solves L z = g, L^T d = z by wave 0 (no barriers: lane l
   //    holds z[l + 64 r]).  The pivot's owner lane scales it by 1 / L_jj and
   //    v_readlane broadcasts it (no LDS round trip on the recurrence); the
@@ -376,6 +473,7 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
       if (lane + 64 * r < P) z[lane + 64 * r] = zr[r];
   }
   __syncthreads();
+#endif
 
   SOLVE_MARK(4)
 #if DLSA_SOLVE_PROFILE

@@ -318,6 +318,23 @@ int dlsa_partition_rows(const int32_t* part_id, int64_t n, int32_t K, int32_t n_
                         int64_t* offsets, int64_t* order, void* stream);
 
 /*
+ * Column moments in HBM -- the device half of Spark's describe(), which the
+ * reference runs over the whole data set to standardise every partition
+ * with the global mean and stddev (projects/logistic_dlsa.py:287-298, read
+ * by dlsa/models.py:99-101):
+ *   out[0 p + j] = count, out[1 p + j] = mean, out[2 p + j] = M2 = sum (x - mean)^2,
+ *   out[3 p + j] = min,   out[4 p + j] = max    of column j of X [n, p] (fp64,
+ * row-major, device; out device [5 p]).  NaN entries are skipped (describe
+ * ignores nulls); a column without values gets count 0 and NaN elsewhere.
+ * Two passes over X (mean, then the squared deviations, compensated sums in
+ * a fixed order: bit-identical run to run); stddev = sqrt(M2 / (count - 1)).
+ * Partial moments of several shards combine exactly by Chan's formula
+ * (dlsa_amd.ingest.merge_moments).  Scratch is allocated on the stream and
+ * freed before return.
+ */
+int dlsa_column_moments(const double* X, int64_t n, int32_t p, double* out, void* stream);
+
+/*
  * Synthetic logistic data in HBM (the input generator of SURVEY 8(d) for
  * configs too large for the host): X[i, j] = u(seed, row0 + i, j) - 0.5 with
  * u a counter-based (splitmix64) U[0,1) double; beta* = 1 on the first

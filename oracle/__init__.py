@@ -30,4 +30,5 @@ from .dlsa_oracle import (  # noqa: F401
     dlsa,
     ols_fit,
     logistic_loglik,
+    column_moments,
 )

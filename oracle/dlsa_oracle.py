@@ -281,6 +281,28 @@ def ols_fit(X, y, fit_intercept=False):
     return dict(coef=theta, Sig_inv=G, Sig_invMcoef=G @ theta)
 
 
+def column_moments(X):
+    """[5, p] count, mean, M2, min, max per column, NaNs skipped -- the
+    numbers Spark's ``describe()`` reports (count, mean, stddev = sqrt(M2 /
+    (count - 1)), min, max) for the reference's data_info
+    (projects/logistic_dlsa.py:287-298), as numpy's two-pass mean /
+    variance."""
+    X = np.asarray(X, np.float64)
+    if X.ndim == 1:
+        X = X[:, None]
+    if X.shape[0] == 0:
+        return np.stack([np.zeros(X.shape[1])] + [np.full(X.shape[1], np.nan)] * 4)
+    ok = ~np.isnan(X)
+    cnt = ok.sum(0).astype(np.float64)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        mean = np.where(ok, X, 0.0).sum(0) / cnt
+        m2 = (np.where(ok, X - mean, 0.0) ** 2).sum(0)
+        mn = np.where(cnt > 0, np.nanmin(np.where(ok, X, np.inf), 0), np.nan)
+        mx = np.where(cnt > 0, np.nanmax(np.where(ok, X, -np.inf), 0), np.nan)
+    m2 = np.where(cnt > 0, m2, np.nan)
+    return np.stack([cnt, mean, m2, mn, mx])
+
+
 # --------------------------------------------------------------------------
 # a11: combine
 # --------------------------------------------------------------------------

@@ -401,3 +401,97 @@ def test_bench_host_cores_reports_quota():
     cores, info = b.host_cores()
     assert 1 <= cores <= info["nproc"]
     assert info["affinity"] <= info["nproc"]
+
+
+# ---- data_info: moments merge and the sharded combine ------------------------
+
+def test_merge_moments_and_describe_frame_match_pandas():
+    """merge_moments (Chan) of the [5, p] moments of uneven row blocks equals
+    the moments of the whole; describe_frame is Spark's describe() layout
+    whose count / mean / stddev / min / max equal pandas describe()
+    (projects/logistic_dlsa.py:287-298; models.py:99-101 reads rows 1, 2)."""
+    import pandas as pd
+
+    from dlsa_amd.ingest import describe_frame, merge_moments
+
+    rs = np.random.RandomState(3)
+    X = rs.randn(5003, 4) * [1.0, 1e3, 1e-3, 5.0] + [0.0, -7.0, 0.05, 2.0]
+    X[17, 2] = np.nan
+    cuts = [0, 1, 900, 901, 3000, 5003]
+    parts = [O.column_moments(X[a:b]) for a, b in zip(cuts[:-1], cuts[1:])]
+    whole = O.column_moments(X)
+    got = merge_moments(parts)
+    assert np.array_equal(got[0], whole[0]) and np.array_equal(got[3:], whole[3:])
+    assert np.abs(got[1] - whole[1]).max() <= 1e-14 * np.abs(X[~np.isnan(X)]).max()
+    assert np.allclose(got[2], whole[2], rtol=1e-13, atol=0)
+    cols = ["a", "b", "c", "d"]
+    info = describe_frame(got, cols)
+    assert list(info.columns) == ["summary"] + cols
+    assert info["summary"].tolist() == ["count", "mean", "stddev", "min", "max"]
+    pdd = pd.DataFrame(X, columns=cols).describe()
+    for c in cols:
+        assert int(info[c][0]) == int(pdd[c]["count"])
+        for row, key in ((1, "mean"), (2, "std"), (3, "min"), (4, "max")):
+            assert abs(float(info[c][row]) - pdd[c][key]) <= 1e-12 * max(1.0, abs(pdd[c][key]))
+
+
+def _moments_worker(rank, world, port, X, q):
+    import torch.distributed as dist
+
+    from dlsa_amd.ingest import combine_moments, describe_frame
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    calls = []
+    orig = dist.all_reduce
+
+    def counting(*a, **k):
+        calls.append(1)
+        return orig(*a, **k)
+
+    dist.all_reduce = counting
+    try:
+        # rank r holds rows i % K in its partitions (K = 5: ranks own 2 / 3 partitions)
+        K = 5
+        k0, k1 = rank * K // world, (rank + 1) * K // world
+        mine = X[(np.arange(len(X)) % K >= k0) & (np.arange(len(X)) % K < k1)]
+        tot = combine_moments(O.column_moments(mine), distributed=True)
+    finally:
+        dist.all_reduce = orig
+    q.put((rank, describe_frame(tot, ["u", "v", "w"]).to_numpy().tolist(), len(calls)))
+    dist.destroy_process_group()
+
+
+def test_sharded_describe_gloo_equals_one_rank():
+    """data_info of a sharded data set: every rank's local moments go through
+    ONE all-reduce and merge in rank order -- the frame is identical on both
+    ranks and equal (to the last digits) to the one-rank frame of all rows."""
+    import multiprocessing as mp
+    import socket
+
+    from dlsa_amd.ingest import describe_frame
+
+    rs = np.random.RandomState(8)
+    X = rs.rand(20011, 3) * [1.0, 100.0, 1e-6] - [0.5, 3.0, 0.0]
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_moments_worker, args=(r, 2, port, X, q)) for r in range(2)]
+    for p_ in ps:
+        p_.start()
+    res = sorted(q.get(timeout=120) for _ in range(2))
+    for p_ in ps:
+        p_.join(timeout=60)
+        assert p_.exitcode == 0
+    one = describe_frame(O.column_moments(X), ["u", "v", "w"]).to_numpy()
+    assert res[0][1] == res[1][1]  # bit-identical on every rank
+    assert res[0][2] == 1 and res[1][2] == 1
+    got = np.array(res[0][1], dtype=object)
+    assert (got[:, 0] == one[:, 0]).all() and (got[0] == one[0]).all()
+    for i in range(1, 5):
+        for j in range(1, 4):
+            assert abs(float(got[i, j]) - float(one[i, j])) <= 1e-13 * max(1.0, abs(float(one[i, j])))

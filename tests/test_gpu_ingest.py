@@ -225,3 +225,142 @@ def test_csv_to_config3_fit_needs_no_reference_code(torch_cuda, tmp_path):
         assert np.abs(fit.theta[k].cpu().numpy() - r["coef"]).max() / np.abs(r["coef"]).max() < 1e-8
         assert np.abs(fit.sig_inv[k].cpu().numpy() - r["Sig_inv"]).max() / \
             np.abs(r["Sig_inv"]).max() < 1e-8
+
+
+# ---- data_info on the device (Spark describe(), logistic_dlsa.py:287-298) ------
+
+@pytest.mark.parametrize("n,p", [(10007, 130), (1, 3), (0, 2), (300001, 7)])
+def test_column_moments_vs_oracle(torch_cuda, n, p):
+    """dlsa_column_moments: count / mean / M2 / min / max per column with NaNs
+    skipped, 3 column blocks at p = 130, empty and one-row inputs."""
+    from dlsa_amd.ingest import column_moments
+
+    rs = np.random.RandomState(n + p)
+    X = rs.randn(n, p) * np.linspace(1e-3, 1e3, p) + np.linspace(-5.0, 5.0, p)
+    if n > 10:
+        X[rs.choice(n, 9), rs.choice(p, 9)] = np.nan
+        X[:, 1] = 4.25  # constant column: M2 exactly 0
+    got = column_moments(X)
+    ref = O.column_moments(X)
+    assert np.array_equal(got[0], ref[0])
+    if n == 0:
+        assert np.isnan(got[1:]).all()
+        return
+    assert np.array_equal(got[3:], ref[3:])
+    # compensated sums on the device, numpy's pairwise sums in the oracle:
+    # agreement to a few ulp of the column's magnitude
+    scale = np.nanmax(np.abs(X), axis=0)
+    assert (np.abs(got[1] - ref[1]) <= 1e-14 * scale).all()
+    assert np.allclose(got[2], ref[2], rtol=1e-12, atol=1e-300)
+    if n > 10:
+        assert got[2, 1] == 0.0
+    assert np.array_equal(column_moments(X), got)  # fixed order: bit-identical
+
+
+def test_read_csv_data_info_matches_pandas_describe(torch_cuda, tmp_path):
+    """read_csv_partitioned returns data_info in Spark's describe().toPandas()
+    layout (summary column, string values) over the x columns, the label and
+    partition_id; its numbers equal pandas describe() of the same rows."""
+    import pandas as pd
+
+    from dlsa_amd.ingest import read_csv_partitioned
+
+    rs = np.random.RandomState(12)
+    df = _write_csv(tmp_path / "air.csv", rs, 23456)
+    lay = read_csv_partitioned(str(tmp_path / "air.csv"), "ArrDelay", ["a", "b"], K=7)
+    info = lay["data_info"]
+    assert list(info.columns) == ["summary", "a", "b", "ArrDelay", "partition_id"]
+    assert info["summary"].tolist() == ["count", "mean", "stddev", "min", "max"]
+    ref = df[["a", "b", "ArrDelay"]].dropna().reset_index(drop=True)
+    ref["ArrDelay"] = (ref["ArrDelay"] > 0).astype(float)
+    ref["partition_id"] = (np.arange(len(ref)) % 7).astype(float)
+    pdd = ref.describe()
+    for c in ["a", "b", "ArrDelay", "partition_id"]:
+        assert int(info[c][0]) == int(pdd[c]["count"]) == len(ref)
+        for row, key in ((1, "mean"), (2, "std"), (3, "min"), (4, "max")):
+            assert abs(float(info[c][row]) - pdd[c][key]) <= 1e-13 * max(1.0, abs(pdd[c][key]))
+
+
+def test_standardized_fit_through_device_data_info(torch_cuda, golden_dir):
+    """The golden data_info (numpy mean / stddev(n-1) in the describe layout)
+    equals the device describe() of the fixture's X, and the standardised fit
+    through the device frame (models.py:99-101) matches the reference's
+    standardized_intercept outputs."""
+    import os
+
+    from dlsa_amd.ingest import describe
+    from dlsa_amd.models import logistic_model_batched
+
+    D = np.load(os.path.join(golden_dir, "standardized_intercept.npz"))
+    info = describe(D["X"], ["a", "b", "c", "d", "e"])
+    center = np.array([float(v) for v in info.iloc[1, 1:]])
+    scale = np.array([float(v) for v in info.iloc[2, 1:]])
+    assert np.allclose(center, D["center"], rtol=1e-14, atol=1e-15)
+    assert np.allclose(scale, D["scale"], rtol=1e-14, atol=0)
+    order, off = O.systematic_partition(np.arange(len(D["y"])) % 3)
+    fit = logistic_model_batched(D["X"][order], D["y"][order], off, fit_intercept=True,
+                                 center=center, scale=scale)
+    ref = D["outs"]
+    assert np.abs(fit.theta.cpu().numpy() - ref[:, :, 1]).max() / np.abs(ref[:, :, 1]).max() < 1e-8
+    assert np.abs(fit.sig_inv.cpu().numpy() - ref[:, :, 3:]).max() / np.abs(ref[:, :, 3:]).max() < 1e-8
+
+
+def _ingest_rank(rank, world, port, path, q):
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dlsa_amd.ingest import read_csv_partitioned
+
+        lay = read_csv_partitioned(path, "ArrDelay", ["a", "b"], K=6, rank=rank, world=world)
+        q.put((rank, lay["data_info"].to_numpy().tolist(), lay["partitions"].tolist(),
+               lay["offsets"].tolist(), lay["X"].cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_ingest_two_ranks_same_data_info(torch_cuda, tmp_path):
+    """Two ranks (gloo, one GPU) each ingest their partitions of the CSV
+    (3 of K = 6); the data_info they combine through one all-reduce equals
+    the one-rank frame, and each rank's rows are its partitions' rows."""
+    import multiprocessing as mp
+    import socket
+
+    from dlsa_amd.ingest import read_csv_partitioned
+
+    rs = np.random.RandomState(21)
+    _write_csv(tmp_path / "air.csv", rs, 12000)
+    path = str(tmp_path / "air.csv")
+    one = read_csv_partitioned(path, "ArrDelay", ["a", "b"], K=6)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_ingest_rank, args=(r, 2, port, path, q)) for r in range(2)]
+    for p_ in ps:
+        p_.start()
+    res = sorted((q.get(timeout=180) for _ in range(2)), key=lambda t: t[0])
+    for p_ in ps:
+        p_.join(timeout=60)
+        assert p_.exitcode == 0
+    ref = one["data_info"].to_numpy()
+    assert res[0][1] == res[1][1]
+    got = np.array(res[0][1], dtype=object)
+    assert (got[0] == ref[0]).all()  # counts exact
+    for i in range(1, 5):
+        for j in range(1, ref.shape[1]):
+            assert abs(float(got[i, j]) - float(ref[i, j])) <= 1e-13 * max(1.0, abs(float(ref[i, j])))
+    Xone, off1 = one["X"].cpu().numpy(), one["offsets"]
+    for rank, _, parts, offs, X in res:
+        assert parts == [3 * rank, 3 * rank + 1, 3 * rank + 2]
+        exp = np.concatenate([Xone[off1[k]:off1[k + 1]] for k in parts])
+        assert np.array_equal(X, exp)
+        assert offs == (np.concatenate([[0], np.cumsum([off1[k + 1] - off1[k] for k in parts])])).tolist()

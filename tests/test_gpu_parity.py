@@ -625,6 +625,42 @@ def test_categorical_bit_identical_runs_and_column_ranges(torch_cuda, M):
         assert _rel(f1.sig_inv[k].cpu(), o["Sig_inv"]) < REL
 
 
+def _per_entry(S, R):
+    """max |S_ij - R_ij| / sqrt(R_ii R_jj) (the Sig_inv metric of the Ozaki tests)"""
+    S, R = np.asarray(S, np.float64), np.asarray(R, np.float64)
+    d = np.sqrt(np.abs(np.diag(R)))
+    return float((np.abs(S - R) / np.maximum(np.outer(d, d), 1e-300)).max())
+
+
+def test_categorical_outlier_and_rare_level_per_entry(torch_cuda, M):
+    """Per-partition fixed-point grids: one numeric value 1e6 x the column's
+    range in partition 1 coarsens only partition 1's grid of that column, and
+    a level with 25 rows per partition keeps its small blocks exact.  Every
+    partition's Sig_inv per entry (|dH_ij| / sqrt(H_ii H_jj)) is within 1e-10
+    of the oracle on the dense expansion, and theta within the parity
+    tolerance."""
+    torch = torch_cuda
+    n_k, K = 25000, 4
+    Xn, codes, y, levels = M.simulate_categorical(K * n_k, seed=23, device="cuda")
+    Xn, codes = Xn.clone(), codes.clone()
+    Xn[n_k + 777, 3] = 5e5                  # outlier row in partition 1 (column range 1)
+    c = codes[:, 2]
+    lv = int(levels[2]) - 1                 # factor 2's last dummy level ...
+    c[c == lv] = 1                          # ... made rare: 25 rows per partition
+    rs = np.random.RandomState(5)
+    rows = np.concatenate([k * n_k + rs.choice(n_k, 25, replace=False) for k in range(K)])
+    c[torch.from_numpy(rows).cuda()] = lv
+    off = np.arange(K + 1, dtype=np.int64) * n_k
+    fit = M.logistic_model_batched_categorical(Xn, codes, y, off, levels, fit_intercept=True)
+    assert (fit.status.cpu().numpy() == 0).all(), fit.status
+    X = O.expand_codes(Xn.cpu().numpy(), codes.cpu().numpy(), levels)
+    yh = y.cpu().numpy()
+    for k in range(K):
+        o = O.logistic_fit(X[off[k]:off[k + 1]], yh[off[k]:off[k + 1]], fit_intercept=True)
+        assert _rel(fit.theta[k].cpu(), o["coef"]) < REL, k
+        assert _per_entry(fit.sig_inv[k].cpu().numpy(), o["Sig_inv"]) < 1e-10, k
+
+
 def test_categorical_invalid_code_fails_loudly(torch_cuda, M):
     from dlsa_amd._hip import DlsaHipError
 

@@ -17,6 +17,7 @@ for v in "$@"; do
     cat15) D=DLSA_CAT_ABLATE=15 ;;
     cat16) D=DLSA_CAT_ABLATE=16 ;;
     solveprof) D=DLSA_SOLVE_PROFILE=1 ;;
+    solveblk) D=DLSA_SOLVE_BLOCKED=1 ;;
     cat31) D=DLSA_CAT_ABLATE=31 ;;
     fab1) D=DLSA_FUSED_ABLATE=1 ;;
     wslot3) D=DLSA_WAVE_NSLOT=3 ;;
@@ -26,27 +27,20 @@ for v in "$@"; do
     word) D=DLSA_WAVE_ORDER=1 ;;
     ozprof) D=DLSA_OZ_PROF=1 ;;
     ozcheck) D=DLSA_OZ_CHECK=1 ;;
+    ozs3) D="DLSA_OZ_SCHED=3" ;;
+    ozs4) D="DLSA_OZ_SCHED=4" ;;
+    ozedge1) D="DLSA_OZ_EDGE=1" ;;
+    ozpd0) D="DLSA_OZ_PDMA=0" ;;
+    ozpd0prof) D="DLSA_OZ_PDMA=0 -DDLSA_OZ_PROF=1" ;;
+    ozpd2) D="DLSA_OZ_PDMA=2" ;;
+    ozpd3) D="DLSA_OZ_PDMA=3" ;;
+    ozpd2prof) D="DLSA_OZ_PDMA=2 -DDLSA_OZ_PROF=1" ;;
+    ozovl) D="DLSA_OZ_OVL=1" ;;
+    ozquad) D="DLSA_OZ_R4=0 -DDLSA_OZ_EDGE=0" ;;
     knobs) D=DLSA_ENV_KNOBS=1 ;;
     ozs1) D=DLSA_OZ_SCHED=1 ;;
-    oz4d) D="DLSA_OZ_DIGITS=4 -DDLSA_OZ_DBATCH=0" ;;
-    oz4dprof) D="DLSA_OZ_DIGITS=4 -DDLSA_OZ_DBATCH=0 -DDLSA_OZ_PROF=1" ;;
-    oz4ds1) D="DLSA_OZ_DIGITS=4 -DDLSA_OZ_DBATCH=0" ;;
     ozs2) D=DLSA_OZ_SCHED=2 ;;
-    ozs1prof) D="DLSA_OZ_SCHED=1 -DDLSA_OZ_PROF=1" ;;
-    ozold) D="DLSA_OZ_MAGICF=0 -DDLSA_OZ_SCHED=0 -DDLSA_OZ_DBATCH=0" ;;
-    ozs0) D="DLSA_OZ_SCHED=0" ;;
-    ozdb0) D="DLSA_OZ_DBATCH=0" ;;
-    ozm0) D="DLSA_OZ_MAGICF=0" ;;
-    ozoldprof) D="DLSA_OZ_MAGICF=0 -DDLSA_OZ_PROF=1" ;;
-    ozdb) D="DLSA_OZ_DBATCH=1" ;;
-    ozs1db) D="DLSA_OZ_SCHED=1 -DDLSA_OZ_DBATCH=1" ;;
-    ozs2prof) D="DLSA_OZ_SCHED=2 -DDLSA_OZ_PROF=1" ;;
     oz6) D=DLSA_OZ_LEVELS=6 ;;
-    oztick0) D=DLSA_OZ_TICK=0 ;;
-    ozprio0) D=DLSA_OZ_PRIO=0 ;;
-    ozab1) D="DLSA_OZ_ABLATE=1 -DDLSA_OZ_PROF=1" ;;
-    ozab2) D="DLSA_OZ_ABLATE=2 -DDLSA_OZ_PROF=1" ;;
-    ozab3) D="DLSA_OZ_ABLATE=3 -DDLSA_OZ_PROF=1" ;;
     nt) D=DLSA_X_DMA_AUX=2 ;;
     dma0) D=DLSA_X_DMA_AUX=0 ;;
     sc1) D=DLSA_X_DMA_AUX=1 ;;
@@ -55,6 +49,7 @@ for v in "$@"; do
   ONLY=None
   case $v in
     oz*|ozs*) ONLY='["irls_oz.hip", "irls_oz_g2.hip"]' ;;
+    solve*) ONLY='["newton_solve.hip"]' ;;
     ols*|wslot3) ONLY='["irls_wave.hip", "irls_wave_g2.hip"]' ;;
   esac
   python -c "from dlsa_amd.build import build; print(build(force=True, out='var/libdlsa_hip_$v.so', defines='$D'.replace('-D', '').split(), only=$ONLY))"

@@ -6,7 +6,8 @@ all in one process on one GPU (rule: interleaved rounds, same device).
         [--libs base,ablate1,...] [--knobs "DLSA_WAVES_F32=8;DLSA_WAVES_F32=4"]
 
 Variants are the .so files tools/build_variants.sh produces
-(dlsa_amd/libdlsa_hip.so = base, tools/_variants/libdlsa_hip_<name>.so).
+(dlsa_amd/libdlsa_hip.so = base, var/libdlsa_hip_<name>.so; host knobs need a
+`knobs` build, -DDLSA_ENV_KNOBS=1).
 Prints one JSON line per (variant, knob) with the median fp32-/fp64-pass time
 and the algorithmic GB/s (n (8p+8) bytes per pass).
 """
@@ -72,7 +73,7 @@ def main():
     libs = {}
     for name in args.libs.split(","):
         path = _hip.LIB_PATH if name == "base" else os.path.join(
-            ROOT, "tools", "_variants", f"libdlsa_hip_{name}.so")
+            ROOT, "var", f"libdlsa_hip_{name}.so")
         libs[name] = load_variant(path)
     knobs = [("" if k.strip() == "default" else k) for k in args.knobs.split(";") if k.strip()] or [""]
     bytes_per_pass = n * (8 * p + 8)
@@ -113,20 +114,23 @@ def main():
                 for kv in [x for x in kn.split(",") if x]:
                     os.environ.pop(kv.split("=")[0], None)
                 # profiling builds (DLSA_OZ_PROF): exact-pass stamp sums per 32-row block
-                prof = [0] * 16
+                prof = [0] * 32
                 for fn in ("dlsa_oz_prof_read", "dlsa_oz_prof_read_g2"):
                     if hasattr(lib, fn):
-                        buf = (ctypes.c_ulonglong * 16)()
+                        buf = (ctypes.c_ulonglong * 32)()
                         getattr(lib, fn)(buf)
                         prof = [a + b for a, b in zip(prof, buf)]
                 if any(prof):
-                    nit = max(1, n // 64 * max(1, s.passes_fp64))  # 64-row iterations
+                    # per-wave sums over all workgroups -> cycles per 64-row iteration
+                    nit = max(1, n // 64 * max(1, s.passes_fp64))
                     d.setdefault("prof", []).append(
-                        {"producer": {k: round(prof[i] / nit, 1)
-                                      for i, k in enumerate(["barrier", "row", "digits"])},
-                         "consumer": {k: round(prof[8 + i] / nit, 1)
-                                      for i, k in enumerate(["barrier", "issue", "mfma",
-                                                             "vmwait"])}})
+                        {**{f"producer{w}": {k: round(prof[4 * w + i] / nit, 1)
+                                             for i, k in enumerate(["barrier", "row", "digits"])}
+                            for w in range(4)},
+                         **{f"consumer{w}": {k: round(prof[16 + 4 * w + i] / nit, 1)
+                                             for i, k in enumerate(["barrier", "issue", "mfma",
+                                                                    "vmwait"])}
+                            for w in range(4)}})
     for (name, kn), d in res.items():
         out = {"lib": name, "knobs": kn, "n": n, "p": p, "K": K, "passes": d["it"][-1]}
         for key in ("f32", "f64"):
