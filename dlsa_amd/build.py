@@ -32,21 +32,48 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found (ROCm >= 7 required)")
 
 
+def _common_flags() -> list:
+    return [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
+            "-Wno-unused-function", "-Wno-unused-command-line-argument",
+            "-I" + os.path.join(ROOT, "include")]
+
+
+def _toolchain_key() -> str:
+    """Target architecture + a hash of the compile flags and the resolved
+    compiler / ROCm install: objects and the library built under another key
+    are not reused."""
+    import hashlib
+    h = hashlib.sha1("\0".join(_common_flags() + [os.path.realpath(hipcc()),
+                                                  os.path.realpath("/opt/rocm")]).encode())
+    return f"{ARCH}-{h.hexdigest()[:12]}"
+
+
+BUILD_DIR = os.path.join(ROOT, "build")
+STAMP = os.path.join(BUILD_DIR, "libdlsa_hip.key")  # toolchain key of the in-tree .so
+
+
 def _stale() -> bool:
     if not os.path.exists(OUT):
+        return True
+    try:
+        with open(STAMP) as f:
+            if f.read().strip() != _toolchain_key():
+                return True
+    except OSError:
         return True
     t = os.path.getmtime(OUT)
     deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [__file__]
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-OBJ_CACHE = os.path.join(ROOT, "build", "obj")
+def _obj_cache() -> str:
+    return os.path.join(BUILD_DIR, "obj", _toolchain_key())
 
 
 def _cached_object(src: str) -> str | None:
-    """The object of `src` from the last product build (no defines), if it is
-    newer than the source and every header."""
-    obj = os.path.join(OBJ_CACHE, os.path.splitext(src)[0] + ".o")
+    """The object of `src` from the last product build (no defines) under the
+    current toolchain key, if it is newer than the source and every header."""
+    obj = os.path.join(_obj_cache(), os.path.splitext(src)[0] + ".o")
     if not os.path.exists(obj):
         return None
     t = os.path.getmtime(obj)
@@ -66,9 +93,7 @@ def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()
     import tempfile
     from concurrent.futures import ThreadPoolExecutor
 
-    common = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
-              "-Wall", "-Wno-unused-function", "-Wno-unused-command-line-argument",
-              "-I" + os.path.join(ROOT, "include")]
+    common = [hipcc()] + _common_flags()
     product = out == OUT and not defines
     jobs = int(os.environ.get("DLSA_BUILD_JOBS", min(8, os.cpu_count() or 1)))
     with tempfile.TemporaryDirectory(prefix="dlsa_build_") as tmp:
@@ -95,10 +120,11 @@ def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()
                 sys.stderr.write(res.stdout + res.stderr)
                 raise RuntimeError(f"hipcc failed on {obj} ({res.returncode})")
         if product:  # keep the objects for variant builds
-            os.makedirs(OBJ_CACHE, exist_ok=True)
+            cache = _obj_cache()
+            os.makedirs(cache, exist_ok=True)
             for obj, res in results:
                 if res is not None:
-                    shutil.copy2(obj, os.path.join(OBJ_CACHE, os.path.basename(obj)))
+                    shutil.copy2(obj, os.path.join(cache, os.path.basename(obj)))
         cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC",
                *[o for o, _ in results], "-o", out + ".tmp"]
         if verbose:
@@ -117,6 +143,10 @@ def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()
         sys.stderr.write(chk.stderr)
         raise RuntimeError(f"{out}.tmp does not load (unresolved symbols)")
     os.replace(out + ".tmp", out)
+    if out == OUT and not defines:
+        os.makedirs(BUILD_DIR, exist_ok=True)
+        with open(STAMP, "w") as f:
+            f.write(_toolchain_key() + "\n")
     return out
 
 

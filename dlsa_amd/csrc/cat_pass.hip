@@ -156,6 +156,10 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
     int cv[FM];
 #pragma unroll
     for (int f = 0; f < FM; ++f) cv[f] = f < F ? (int)cr[f] : 0;
+    // y with the row's x and codes, one memory round trip per row (left to the
+    // compiler, its load sinks below the exp and costs a second round trip)
+    double yv = a.y[row];
+    asm volatile("" : "+v"(yv));
 
     double e0 = 0.0, e1 = 0.0;
 #pragma unroll
@@ -169,7 +173,6 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
     for (int f = 0; f < FM; ++f)
       if (f < F && cv[f] > 0) e0 += th[t_doff[f] + cv[f] - 1];
     const double e = e0 + e1;
-    const double yv = a.y[row];
     const double ea = exp(-fabs(e));
     const double inv = 1.0 / (1.0 + ea);
     const double mu = e >= 0.0 ? inv : ea * inv;
@@ -320,95 +323,126 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
 }
 
 // Level presence per chunk: counts[chunk, d] = 1 if a row of the chunk
-// selects dummy column d (presence flags: plain LDS stores of 1, no atomics);
-// bad[chunk] = codes outside 0..L_f-1; colmax[chunk, i] = max |x_i| over the
-// finite values of the chunk (raw numeric columns: the fixed-point grids).
-// One streaming read of the chunk's codes and numeric columns with
-// wave-contiguous loads: each wave takes windows of F dwords (q doubles) per
-// lane, so the factor of every code byte (the column of every value) is
-// fixed per lane and load slot -- the maxima stay in registers until one LDS
-// max per lane and slot (|x| >= 0 orders like its bits as uint64).
-__global__ __launch_bounds__(256) void cat_presence_kernel(const CatArgs a, int32_t* counts,
+// selects dummy column d; bad[chunk] = codes outside 0..L_f-1; colmax[chunk,
+// i] = max |x_i| over the finite values of the chunk (raw numeric columns:
+// the fixed-point grids).  The outputs are zeroed by the launcher.
+// A streaming pass, latency-bound unless many loads are in flight: each
+// chunk is split over S workgroups (contiguous row ranges, ~16 per CU in
+// total); every load is unconditional (out-of-range lanes load a clamped
+// in-range address and discard it -- a predicated load puts each load in its
+// own branch region, each closed by a vmcnt(0) wait); the codes are read as
+// 16-byte units (4 per lane in flight, the factor of each byte advanced
+// incrementally from one 32-bit modulo per unit) and the numeric columns as
+// wave-contiguous windows of q doubles per lane, two windows (2 QS loads) in
+// flight, so the column of every value is fixed per lane and slot and the
+// maxima stay in registers (|x| >= 0 orders like its bits as uint64).
+// Flags: plain LDS stores of 1, then plain global stores of 1.
+template <int QS>
+__global__ __launch_bounds__(256) void cat_presence_kernel(const CatArgs a, int S, int32_t* counts,
                                                            int32_t* bad, double* colmax) {
   __shared__ int32_t flag[kCatPMax];
   __shared__ int32_t nbad;
   __shared__ unsigned long long cmax[kCatQMax];
-  __shared__ int32_t t_nlev[kCatMaxFactors], t_doff[kCatMaxFactors];
-  const int chunk = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  __shared__ int32_t t_nd[kCatMaxFactors];  // nlev | doff << 16
+  const int chunk = blockIdx.x / S, sub = blockIdx.x - chunk * S;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int F = a.F, q = a.q;
   const int D = a.P - a.intercept - q;
   const int doff0 = a.intercept + q;
   for (int i = tid; i < kCatPMax; i += 256) flag[i] = 0;
   if (tid < kCatQMax) cmax[tid] = 0ull;
-  if (tid < kCatMaxFactors) {
-    t_nlev[tid] = a.nlev[tid];
-    t_doff[tid] = a.doff[tid] - doff0;
-  }
+  if (tid < kCatMaxFactors) t_nd[tid] = a.nlev[tid] | ((a.doff[tid] - doff0) << 16);
   if (tid == 0) nbad = 0;
   __syncthreads();
-  const int64_t row0 = a.chunk_row0[chunk];
   const int nrows = a.chunk_rows[chunk];
+  const int rps = (nrows + S - 1) / S;
+  const int r_begin = min(nrows, sub * rps), r_end = min(nrows, r_begin + rps);
+  const int64_t row0 = a.chunk_row0[chunk] + r_begin;
+  const int rows = r_end - r_begin;
 
-  // ---- codes: bytes [row0 F, (row0 + nrows) F), read as aligned dwords -----
-  if (F > 0) {
+  // ---- codes: bytes [row0 F, (row0 + rows) F) as aligned 16-byte units ------
+  if (F > 0 && rows > 0) {
     const uintptr_t cb = (uintptr_t)(a.codes + row0 * F);
-    const uintptr_t base = cb & ~(uintptr_t)3;
-    const int skew = (int)(cb - base);
-    const int64_t nbytes = (int64_t)nrows * F;
-    const int64_t wstride = 4LL * F * 256;  // bytes per workgroup iteration (a multiple of F)
+    const uint4* base = (const uint4*)(cb & ~(uintptr_t)15);
+    const int skew = (int)(cb & 15);
+    const int nbytes = rows * F;
+    const int nunits = (skew + nbytes + 15) >> 4;
+    constexpr int U = 4;
     int nb = 0;
-    for (int64_t o0 = (int64_t)wid * F * 256; o0 < skew + nbytes; o0 += wstride) {
-      for (int s = 0; s < F; ++s) {
-        const int64_t o = o0 + s * 256 + 4 * lane;  // byte offset from base of this dword
-        if (o >= skew + nbytes || o + 4 <= skew) continue;
-        const uint32_t word = *(const uint32_t*)(base + o);
+    for (int u0 = tid; u0 < nunits; u0 += 256 * U) {
+      uint4 w[U];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int64_t b = o + j - skew;  // byte index in the chunk's codes
-          if (b < 0 || b >= nbytes) continue;
-          const int f = (int)(b % F);
-          const int c = (word >> (8 * j)) & 0xFF;
-          if (c > t_nlev[f])
-            ++nb;
-          else if (c > 0)
-            flag[t_doff[f] + c - 1] = 1;
+      for (int k = 0; k < U; ++k) w[k] = base[min(u0 + 256 * k, nunits - 1)];
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const int u = u0 + 256 * k;
+        const int b0 = 16 * u - skew;  // chunk byte of the unit's first byte
+        int f = (int)((unsigned)(b0 + 16 * F) % (unsigned)F);
+        const uint32_t ws[4] = {w[k].x, w[k].y, w[k].z, w[k].w};
+        const bool unit_in = u < nunits;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int b = b0 + i;
+          const int c = (ws[i >> 2] >> (8 * (i & 3))) & 0xFF;
+          const int nd = t_nd[f];
+          const bool in = unit_in && (unsigned)b < (unsigned)nbytes;
+          const bool isbad = in && c > (nd & 0xFFFF);
+          nb += isbad ? 1 : 0;
+          if (in && !isbad && c > 0) flag[(nd >> 16) + c - 1] = 1;
+          f = f + 1 == F ? 0 : f + 1;
         }
       }
     }
     if (nb) atomicAdd(&nbad, nb);
   }
 
-  // ---- numeric columns: doubles [row0 q, (row0 + nrows) q) -------------------
-  if (q > 0) {
+  // ---- numeric columns: doubles [row0 q, (row0 + rows) q) -------------------
+  if (q > 0 && rows > 0) {
     const double* xb = a.Xn + row0 * q;
-    const int64_t ne = (int64_t)nrows * q;
-    const int64_t wstride = 4LL * q * 64;  // doubles per workgroup iteration (a multiple of q)
-    double mx[kCatQMax];
+    const int64_t ne = (int64_t)rows * q;
+    const int64_t wstride = 4LL * q * 64;  // doubles per workgroup window (a multiple of q)
+    unsigned long long mx[QS];  // max |x| as bits (|x| >= 0 orders like its bits)
 #pragma unroll
-    for (int s = 0; s < kCatQMax; ++s) mx[s] = 0.0;
-    for (int64_t e0 = (int64_t)wid * q * 64; e0 < ne; e0 += wstride) {
+    for (int s = 0; s < QS; ++s) mx[s] = 0ull;
+    for (int64_t e0 = (int64_t)wid * q * 64; e0 < ne; e0 += 2 * wstride) {
+      double v[2][QS];
 #pragma unroll
-      for (int s = 0; s < kCatQMax; ++s) {
-        if (s < q) {
-          const int64_t e = e0 + s * 64 + lane;
-          if (e < ne) {
-            const double x = xb[e];
-            // finite values only: a NaN / Inf row fails its own partition
-            if (isfinite(x)) mx[s] = fmax(mx[s], fabs(x));
-          }
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int s = 0; s < QS; ++s) {
+          const int64_t e = e0 + h * wstride + s * 64 + lane;
+          v[h][s] = __builtin_nontemporal_load(xb + ((s < q && e < ne) ? e : 0));
         }
-      }
+      // every load used unconditionally (no load sunk into a branch of its own)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int s = 0; s < QS; ++s) asm volatile("" : "+v"(v[h][s]));
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int s = 0; s < QS; ++s) {
+          const int64_t e = e0 + h * wstride + s * 64 + lane;
+          // finite values only: a NaN / Inf row fails its own partition
+          const unsigned long long u =
+              (unsigned long long)__double_as_longlong(v[h][s]) & 0x7FFFFFFFFFFFFFFFull;
+          const bool ok = s < q && e < ne && u < 0x7FF0000000000000ull;
+          mx[s] = max(mx[s], ok ? u : 0ull);
+        }
     }
 #pragma unroll
-    for (int s = 0; s < kCatQMax; ++s)
+    for (int s = 0; s < QS; ++s)
       if (s < q)
-        __hip_atomic_fetch_max(&cmax[(s * 64 + lane) % q], (unsigned long long)__double_as_longlong(mx[s]),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_max(&cmax[(s * 64 + lane) % q], mx[s], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   __syncthreads();
-  for (int d = tid; d < D; d += 256) counts[(int64_t)chunk * D + d] = flag[d];
-  if (tid == 0) bad[chunk] = nbad;
-  if (tid < q) colmax[(int64_t)chunk * kCatQMax + tid] = __longlong_as_double((long long)cmax[tid]);
+  for (int d = tid; d < D; d += 256)
+    if (flag[d]) counts[(int64_t)chunk * D + d] = 1;
+  if (tid == 0 && nbad) atomicAdd(&bad[chunk], nbad);
+  if (tid < q && cmax[tid])
+    __hip_atomic_fetch_max((unsigned long long*)&colmax[(int64_t)chunk * kCatQMax + tid], cmax[tid],
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Per partition: a selected dummy level with no rows -> the reference's
@@ -497,8 +531,17 @@ hipError_t launch_cat_pass(const CatArgs& a, bool standardize, int n_chunks, hip
 hipError_t launch_cat_presence(const CatArgs& a, int n_chunks, int32_t* counts, int32_t* bad,
                                double* colmax, hipStream_t s) {
   if (n_chunks <= 0) return hipSuccess;
-  hipLaunchKernelGGL(cat_presence_kernel, dim3(n_chunks), dim3(256), 0, s, a, counts, bad,
-                     colmax);
+  const int D = a.P - a.intercept - a.q;
+  hipError_t e = hipMemsetAsync(counts, 0, 4LL * n_chunks * std::max(D, 1), s);
+  if (e == hipSuccess) e = hipMemsetAsync(bad, 0, 4LL * n_chunks, s);
+  if (e == hipSuccess) e = hipMemsetAsync(colmax, 0, 8LL * kCatQMax * n_chunks, s);
+  if (e != hipSuccess) return e;
+  // ~16 workgroups per CU in total (a streaming pass: loads in flight)
+  const int S = std::max(1, std::min(64, (4096 + n_chunks - 1) / n_chunks));
+  auto kern = a.q <= 4 ? cat_presence_kernel<4>
+              : a.q <= 8 ? cat_presence_kernel<8>
+              : a.q <= 12 ? cat_presence_kernel<12> : cat_presence_kernel<16>;
+  hipLaunchKernelGGL(kern, dim3(n_chunks * S), dim3(256), 0, s, a, S, counts, bad, colmax);
   return hipGetLastError();
 }
 

@@ -264,6 +264,11 @@ __device__ __forceinline__ void store_tiles(Acc (&acc)[(CG<NT, W>::TPW)], double
   });
 }
 
+// Profiling-only A/B (tools/build_variants.sh cmabl; product 0): the CM & 1
+// pass skips its per-value max |x| update (the record reads 0).
+#ifndef DLSA_CM_ABLATE
+#define DLSA_CM_ABLATE 0
+#endif
 // CM (bits): also record the chunk's per-feature max |x| into a.colmax (1:
 // the fit's first full-data bf16 pass) and max |z| (z = sqrt(w) x, the fp32
 // value of the bf16 image) into a.zcolmax (2: the bf16 passes of partitions
@@ -413,7 +418,8 @@ void irls_coop_kernel(const PassArgs a) {
         if constexpr (STD) v = (v - stdv[sl + LPR * m]) * stdv[G::PMAX + sl + LPR * m];
         if (m == 0 && ic && sl == 0) v = 1.0;
         xv[m] = v;
-        if constexpr (CM & 1) cmx[m] = max(cmx[m], (uint32_t)__double2hiint(v) & 0x7FFFFFFFu);
+        if constexpr ((CM & 1) && !DLSA_CM_ABLATE)
+          cmx[m] = max(cmx[m], (uint32_t)__double2hiint(v) & 0x7FFFFFFFu);
         if (m & 1)
           e1 = fma(v, beta[m], e1);
         else

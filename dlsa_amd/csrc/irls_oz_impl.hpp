@@ -305,8 +305,13 @@ __device__ __forceinline__ int digit_exponent(uint32_t xhi, uint32_t zbits, doub
     bound = fmin(bound, 0.5 * xb);  // (also when growth overflowed to inf)
   }
   const int e = __builtin_amdgcn_frexp_exp(bound);
-  return min(max(e, EMIN), EMAX);
+  return max(e, EMIN);  // above EMAX: the caller fails the chunk (digit_overflow)
 }
+// |z| >= 2^EMAX: the digits of F = round(z 2^(38 - E)) would wrap at the
+// clamped exponent (a finite, wrong Hessian), so such a chunk publishes a NaN
+// log-likelihood instead -- the partition then fails as nonfinite, as the
+// fp64 Gram's inf would make it
+__device__ __forceinline__ bool digit_overflow(int e) { return e > EMAX; }
 
 }  // namespace ozk
 
@@ -832,6 +837,7 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
   // in a fixed order, so every thread forms the same growth factor
   double dth = 0.0;
   uint32_t xh = 0;
+  bool e_ovf = false;
   if (tid < PMAX) {
     const double th = (tid < P) ? a.theta[(int64_t)part * P + tid] : 0.0;
     bet[tid] = th;
@@ -865,13 +871,15 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
       xm = max(xm, xred[w]);
     }
     const double growth = exp(0.5 * sd * ozk::xbound(xm)) * (1.0 + 0x1p-40);
-    ex[tid] = digit_exponent(a.colmax[(int64_t)chunk * PMAX + tid],
-                             a.zcolmax[(int64_t)chunk * PMAX + tid], growth,
-                             FAM == FAMILY_LOGISTIC);
+    const int e = digit_exponent(a.colmax[(int64_t)chunk * PMAX + tid],
+                                 a.zcolmax[(int64_t)chunk * PMAX + tid], growth,
+                                 FAM == FAMILY_LOGISTIC);
+    ex[tid] = min(e, ozk::EMAX);
+    e_ovf = ozk::digit_overflow(e);
   }
   // (the ring needs no zeroing: past-the-chunk rows are zeroed in registers
   // and nothing reads a slot's bytes that the DMA did not write)
-  __syncthreads();
+  const bool chunk_ovf = __syncthreads_or(e_ovf) != 0;
 
   auto slot_x = [&](int blk) -> char* {
     const uintptr_t start = (uintptr_t)(a.X + (row0 + (int64_t)blk * RB) * p);
@@ -1313,7 +1321,7 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
     double s = 0.0;
 #pragma unroll
     for (int w = 0; w < NPW; ++w) s += red[w * (PMAX + 1) + PMAX];
-    a.slab_ll[chunk] = s;
+    a.slab_ll[chunk] = chunk_ovf ? __builtin_nan("") : s;
   }
 }
 

@@ -253,18 +253,15 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
   // (w' = w in slot order), and those of an active column are A * Sign
   // exactly (Sigma_AA w = A Sigma_AA Sigma_AA^-1 Sign): (m - |A|) |A|
   // multiply-adds per knot.  Adding a variable writes one column (its row of
-  // the symmetric Sigma); a lasso drop moves the last slot's column into the
-  // freed one -- no permutation of the whole matrix (the column swaps of
-  // round 2 touched two strided columns per added variable and re-sorted every
-  // active column after a drop).
+  // the symmetric Sigma); a lasso drop (rare) compacts the kept columns into
+  // slots 0..|A|-1 in active order, so slot[q] = q always and every dot
+  // product sums in active order (the column swaps of round 2 touched two
+  // strided columns per added variable).
   std::vector<double> SA((size_t)m * m, 0.0);
   std::vector<int> slot;
   auto put_col = [&](int s_, int var) {
     const double* src = &Sig[(size_t)var * m];
     for (int i = 0; i < m; ++i) SA[(size_t)i * m + s_] = src[i];
-  };
-  auto move_col = [&](int from, int to) {
-    for (int i = 0; i < m; ++i) SA[(size_t)i * m + to] = SA[(size_t)i * m + from];
   };
 
   std::vector<double> Cvec(m, 0.0);
@@ -476,22 +473,6 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
       rank = R.d;
       R.rebuild_lt();
       u_valid = false;
-      // free the dropped slots: the column of the highest used slot moves in
-      int used = na;
-      for (int q = 0; q < na; ++q) {
-        if (!drops[q]) continue;
-        const int s_ = slot[q], last = used - 1;
-        if (s_ != last) {
-          for (int q2 = 0; q2 < na; ++q2)
-            if (slot[q2] == last) {
-              move_col(last, s_);
-              slot[q2] = s_;
-              break;
-            }
-        }
-        slot[q] = -1;
-        --used;
-      }
       std::vector<int> na_active, na_slot;
       std::vector<double> na_sign;
       for (int q = 0; q < na; ++q) {
@@ -505,8 +486,20 @@ extern "C" int dlsa_lars_lsa(const double* Sigma0, const double* b0, int32_t P,
         }
       }
       active.swap(na_active);
-      slot.swap(na_slot);
       Sign.swap(na_sign);
+      // renumber the kept columns' slots in active order (slot[q] = q): the
+      // dot products of dots_rows then sum in active order after a drop too,
+      // the same order as a run without drops
+      {
+        const int na2 = (int)active.size();
+        std::vector<double> tmp((size_t)m * na2);
+        for (int i = 0; i < m; ++i)
+          for (int q = 0; q < na2; ++q) tmp[(size_t)i * na2 + q] = SA[(size_t)i * m + na_slot[q]];
+        for (int i = 0; i < m; ++i)
+          for (int q = 0; q < na2; ++q) SA[(size_t)i * m + q] = tmp[(size_t)i * na2 + q];
+        slot.resize(na2);
+        for (int q = 0; q < na2; ++q) slot[q] = q;
+      }
     }
   }
 

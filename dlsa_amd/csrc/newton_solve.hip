@@ -23,15 +23,6 @@
 #ifndef DLSA_SOLVE_PROFILE
 #define DLSA_SOLVE_PROFILE 0
 #endif
-// Blocked triangular solves (DLSA_SOLVE_BLOCKED 1): the Cholesky keeps the
-// inverse of each 16x16 diagonal block in place of the block, the panel
-// below is A_ib Linv_bb^T (16 independent dot products per row instead of a
-// 16-step substitution) and both triangular solves run a block at a time
-// (16 lanes apply Linv_bb, every thread updates its rows) -- 2 NT barrier
-// steps instead of 2 P dependent ones.  0: the per-column solves.
-#ifndef DLSA_SOLVE_BLOCKED
-#define DLSA_SOLVE_BLOCKED 0
-#endif
 #if DLSA_SOLVE_PROFILE
 #define SOLVE_MARK(i) \
   if (k == 0 && tid == 0) tmark[i] = clock64();
@@ -81,11 +72,16 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
   const int lane = tid & 63, wid = tid >> 6;
   if (a.status[k] != STATUS_RUNNING) return;  // block-uniform
   const int P = a.P;
-  double* H = sm;                    // packed lower triangle, P (P + 1) / 2
+  double* dblk = sm;                 // [16][16]: the panel's L_bb (strict lower), 1 / L_kk
+                                     // on the diagonal, at LDS offset 0: compile-time
+                                     // addresses in the panel solve (packed-triangle
+                                     // addresses of a moving panel, or a P-dependent base,
+                                     // cost ~140 spilled SGPRs)
+  double* H = sm + 256;              // packed lower triangle, P (P + 1) / 2
   double* g = H + P * (P + 1) / 2;   // PP
   double* z = g + PP;                // PP
   double* invd = z + PP;             // PP: 1 / L_jj
-  double* red = invd + PP;           // 8: [0..3] block reductions, [5] flag, [7] ll
+  double* red = invd + PP;           // 8: [0..3] block reductions, [5] flag, [6] store sink, [7] ll
 
   // chunk partials were summed into the partition's first chunk by
   // partials_sum_kernel (fixed chunk order)
@@ -93,6 +89,15 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
   const int phase = a.phase[k];
 #if DLSA_SOLVE_PROFILE
   long long tmark[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  long long tpan[3] = {0, 0, 0}, tp0 = 0;  // Cholesky: diagonal block, panel rows, trailing
+#define SOLVE_PAN(i)                             \
+  if (k == 0 && tid == 0) {                      \
+    const long long tn = clock64();              \
+    if (i > 0) tpan[i - 1] += tn - tp0;          \
+    tp0 = tn;                                    \
+  }
+#else
+#define SOLVE_PAN(i)
 #endif
   SOLVE_MARK(0)
 
@@ -207,12 +212,24 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
     const int c0 = 16 * b;
     if (c0 >= P) break;
     const int nb = min(16, P - c0);
+    SOLVE_PAN(0)
+    // the lane index re-defined opaquely per panel: otherwise the compiler
+    // hoists the ~40 lane-compare masks of the loop body out of the panel
+    // loop and spills them (~140 SGPRs, a v_readlane per reload)
+    int lv = lane;
+    asm volatile("" : "+v"(lv));
     if (wid == 0) {
-      const int i = lane & 15;
-      const bool act = lane < nb;
+      const int i = lv & 15;
+      const bool act = lv < nb;
+      // branch-free: every lane loads an in-triangle address (clamped) and
+      // selects; lanes / entries outside the block store to a dummy slot
+      const int ri = min(c0 + i, P - 1);
       double av[16];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) av[j] = (act && j <= i) ? H[tri(c0 + i, c0 + j)] : 0.0;
+      for (int j = 0; j < 16; ++j) {
+        const double hv = H[tri(ri, min(c0 + j, ri))];
+        av[j] = (act && j <= i) ? hv : 0.0;
+      }
       bool good = true;
       double ild = 0.0;  // lane kk: 1 / L_kk
 #pragma unroll
@@ -222,44 +239,26 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
           good = good && dkk > 0.0 && isfinite(dkk);
           const double lkk = sqrt(dkk);
           const double il = 1.0 / lkk;
-          if (lane == kk) ild = il;
+          if (lv == kk) ild = il;
           av[kk] = (i > kk) ? av[kk] * il : (i == kk ? lkk : av[kk]);
 #pragma unroll
           for (int j = kk + 1; j < 16; ++j) {
             const double ljk = readlane_f64(av[kk], j);  // L[j][kk], row j's lane
             if (j <= i) av[j] = fma(-av[kk], ljk, av[j]);
           }
-          if (lane == 0) invd[c0 + kk] = il;
+          if (lv == 0) invd[c0 + kk] = il;
         }
       }
-#if DLSA_SOLVE_BLOCKED
-      // Linv = L_bb^-1, lower: lane j (< nb) solves column j, L_bb entries
-      // broadcast from their rows' lanes; stored over L_bb
-      {
-        const int j = lane;
-        double x[16];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          x[r] = 0.0;
-          if (r < nb) {  // wave-uniform
-            double acc = (r == j) ? 1.0 : 0.0;
+      for (int j = 0; j < 16; ++j) *((act && j <= i) ? H + tri(ri, c0 + j) : red + 6) = av[j];
+      if (lv < 16) {
 #pragma unroll
-            for (int k = 0; k < r; ++k) acc = fma(-readlane_f64(av[k], r), x[k], acc);
-            x[r] = acc * readlane_f64(ild, r);
-          }
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (j < nb && r >= j && r < nb) H[tri(c0 + r, c0 + j)] = x[r];
+        for (int j = 0; j < 16; ++j) dblk[16 * lv + j] = j < i ? av[j] : (j == i ? ild : 0.0);
       }
-#else
-#pragma unroll
-      for (int j = 0; j < 16; ++j)
-        if (act && j <= i) H[tri(c0 + i, c0 + j)] = av[j];
-#endif
-      if (lane == 0 && !good) red[5] = 1.0;
+      if (lv == 0 && !good) red[5] = 1.0;
     }
     __syncthreads();
+    SOLVE_PAN(1)
     if (red[5] != 0.0) {  // block-uniform
       ok = false;
       break;
@@ -271,60 +270,53 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
         double x[16];
 #pragma unroll
         for (int kk = 0; kk < 16; ++kk) x[kk] = hr[kk];
-#if DLSA_SOLVE_BLOCKED
-        // L_ib = A_ib Linv_bb^T: 16 independent dot products
-        double o[16];
-#pragma unroll
-        for (int m = 0; m < 16; ++m) {
-          double acc = 0.0;
-#pragma unroll
-          for (int kk = 0; kk <= m; ++kk) acc = fma(x[kk], H[tri(c0 + m, c0 + kk)], acc);
-          o[m] = acc;
-        }
-#pragma unroll
-        for (int kk = 0; kk < 16; ++kk) hr[kk] = o[kk];
-#else
 #pragma unroll
         for (int kk = 0; kk < 16; ++kk) {
-          x[kk] *= invd[c0 + kk];
+          x[kk] *= dblk[17 * kk];
 #pragma unroll
-          for (int m = kk + 1; m < 16; ++m) x[m] = fma(-x[kk], H[tri(c0 + m, c0 + kk)], x[m]);
+          for (int m = kk + 1; m < 16; ++m) x[m] = fma(-x[kk], dblk[16 * m + kk], x[m]);
         }
 #pragma unroll
         for (int kk = 0; kk < 16; ++kk) hr[kk] = x[kk];
-#endif
       }
       __syncthreads();
+      SOLVE_PAN(2)
       const int m = NT - b - 1;  // tile rows below the panel
       const int ntile = m * (m + 1) / 2;
-      const int fl = lane & 15, q = lane >> 4;
+      const int fl = lv & 15, q = lv >> 4;
       for (int t = wid; t < ntile; t += 4) {  // wave-uniform
         int I = 0;
         while ((I + 1) * (I + 2) / 2 <= t) ++I;
         const int J = t - I * (I + 1) / 2;
         const int gI = c0 + 16 * (I + 1), gJ = c0 + 16 * (J + 1);
+        // branch-free as above (clamped in-triangle loads, dummy-slot stores)
         d4s acc;
+        int adr[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = gI + q + 4 * r, col = gJ + fl;
-          acc[r] = (row < P && col <= row) ? H[tri(row, col)] : 0.0;
+          const bool in = row < P && col <= row;
+          const int rc = min(row, P - 1);
+          const double hv = H[tri(rc, min(col, rc))];
+          acc[r] = in ? hv : 0.0;
+          adr[r] = in ? tri(row, col) : -1;
         }
-        const int ra = gI + fl, rb = gJ + fl;
+        const int ra = min(gI + fl, P - 1), rb = min(gJ + fl, P - 1);
+        const bool ina = gI + fl < P, inb = gJ + fl < P;
 #pragma unroll
         for (int st = 0; st < 4; ++st) {
           const int kc = c0 + 4 * st + q;
-          const double x_a = ra < P ? H[tri(ra, kc)] : 0.0;
-          const double x_b = rb < P ? H[tri(rb, kc)] : 0.0;
+          const double ha = H[tri(ra, kc)], hb = H[tri(rb, kc)];
+          const double x_a = ina ? ha : 0.0;
+          const double x_b = inb ? hb : 0.0;
           acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-x_a, x_b, acc, 0, 0, 0);
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = gI + q + 4 * r, col = gJ + fl;
-          if (row < P && col <= row) H[tri(row, col)] = acc[r];
-        }
+        for (int r = 0; r < 4; ++r) *(adr[r] >= 0 ? H + adr[r] : red + 6) = acc[r];
       }
     }
     __syncthreads();
+    SOLVE_PAN(3)
   }
   if (!ok) {
     if (a.subsample) {
@@ -349,56 +341,6 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
   }
 
   SOLVE_MARK(3)
-#if DLSA_SOLVE_BLOCKED
-  // 5. triangular solves L z = g, L^T d = z a 16-block at a time (the
-  //    diagonal blocks hold Linv_bb): 16 lanes of wave 0 apply Linv_bb (or
-  //    its transpose) to the block's right-hand side, then every thread
-  //    updates the remaining entries with the block's off-diagonal L
-  for (int f = tid; f < PP; f += 256) z[f] = f < P ? g[f] : 0.0;
-  __syncthreads();
-  for (int b = 0; b < NT; ++b) {
-    const int c0 = 16 * b;
-    if (c0 >= P) break;
-    const int nb = min(16, P - c0);
-    if (wid == 0) {
-      double acc = 0.0;
-#pragma unroll
-      for (int k = 0; k < 16; ++k)
-        if (k < nb && k <= lane) acc = fma(H[tri(c0 + lane, c0 + k)], z[c0 + k], acc);
-      if (lane < nb) z[c0 + lane] = acc;
-    }
-    __syncthreads();
-    for (int j = c0 + 16 + tid; j < P; j += 256) {
-      double acc = z[j];
-      const double* lr = H + tri(j, c0);
-#pragma unroll
-      for (int k = 0; k < 16; ++k) acc = fma(-lr[k], z[c0 + k], acc);
-      z[j] = acc;
-    }
-    __syncthreads();
-  }
-  for (int b = NT - 1; b >= 0; --b) {
-    const int c0 = 16 * b;
-    if (c0 >= P) continue;
-    const int nb = min(16, P - c0);
-    if (wid == 0) {
-      double acc = 0.0;
-#pragma unroll
-      for (int k = 0; k < 16; ++k)
-        if (k < nb && k >= lane) acc = fma(H[tri(c0 + k, c0 + lane)], z[c0 + k], acc);
-      if (lane < nb) z[c0 + lane] = acc;
-    }
-    __syncthreads();
-    for (int j = tid; j < c0; j += 256) {
-      double acc = z[j];
-#pragma unroll
-      for (int k = 0; k < 16; ++k)
-        if (k < nb) acc = fma(-H[tri(c0 + k, j)], z[c0 + k], acc);
-      z[j] = acc;
-    }
-    __syncthreads();
-  }
-#else
   // 5. triangular solves L z = g, L^T d = z by wave 0 (no barriers: lane l
   //    holds z[l + 64 r]).  The pivot's owner lane scales it by 1 / L_jj and
   //    v_readlane broadcasts it (no LDS round trip on the recurrence); the
@@ -415,13 +357,18 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
       ir[r] = i < P ? invd[i] : 0.0;
     }
     for (int j0 = 0; j0 < P; j0 += U) {
+      // lane index re-defined per step group (no hoisted lane masks to spill);
+      // unconditional in-triangle loads (row clamped to [j, P - 1]) + selects
+      int lv = lane;
+      asm volatile("" : "+v"(lv));
       double hv[U][R];
 #pragma unroll
       for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-          const int i = lane + 64 * r, j = j0 + u;
-          hv[u][r] = (j < P && i > j && i < P) ? H[tri(i, j)] : 0.0;
+          const int i = lv + 64 * r, j = min(j0 + u, P - 1);
+          const double h = H[tri(max(min(i, P - 1), j), j)];
+          hv[u][r] = (j0 + u < P && i > j && i < P) ? h : 0.0;
         }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -434,7 +381,7 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
           const double zj = readlane_f64(zs, j & 63);
 #pragma unroll
           for (int r = 0; r < R; ++r) {  // branch-free: hv = 0 off the active rows
-            const int i = lane + 64 * r;
+            const int i = lv + 64 * r;
             const double upd = fma(-hv[u][r], zj, zr[r]);
             zr[r] = i == j ? zj : upd;
           }
@@ -442,13 +389,16 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
       }
     }
     for (int j0 = P - 1; j0 >= 0; j0 -= U) {
+      int lv = lane;
+      asm volatile("" : "+v"(lv));
       double hv[U][R];
 #pragma unroll
       for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-          const int i = lane + 64 * r, j = j0 - u;
-          hv[u][r] = (j >= 0 && i < j) ? H[tri(j, 0) + i] : 0.0;
+          const int i = lv + 64 * r, j = max(j0 - u, 0);
+          const double h = H[tri(j, 0) + min(i, j)];
+          hv[u][r] = (j0 - u >= 0 && i < j) ? h : 0.0;
         }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -461,7 +411,7 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
           const double zj = readlane_f64(zs, j & 63);
 #pragma unroll
           for (int r = 0; r < R; ++r) {
-            const int i = lane + 64 * r;
+            const int i = lv + 64 * r;
             const double upd = fma(-hv[u][r], zj, zr[r]);
             zr[r] = i == j ? zj : upd;
           }
@@ -473,13 +423,13 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
       if (lane + 64 * r < P) z[lane + 64 * r] = zr[r];
   }
   __syncthreads();
-#endif
 
   SOLVE_MARK(4)
 #if DLSA_SOLVE_PROFILE
   if (k == 0 && tid == 0)
-    printf("[solve-profile] P=%d assemble %lld publish %lld cholesky %lld trisolve %lld\n", P,
-           tmark[1] - tmark[0], tmark[2] - tmark[1], tmark[3] - tmark[2], tmark[4] - tmark[3]);
+    printf("[solve-profile] P=%d assemble %lld publish %lld cholesky %lld (diag %lld panel %lld "
+           "trailing %lld) trisolve %lld\n", P, tmark[1] - tmark[0], tmark[2] - tmark[1],
+           tmark[3] - tmark[2], tpan[0], tpan[1], tpan[2], tmark[4] - tmark[3]);
 #endif
   // 6. update + convergence ------------------------------------------------
   double dm = 0.0, tm = 0.0, tg = 0.0;
@@ -624,7 +574,7 @@ static hipError_t launch_solve_t(const SolveArgs& a, int K, size_t lds, hipStrea
 
 hipError_t launch_newton_solve(const SolveArgs& a, int K, hipStream_t s) {
   const int PP = 16 * a.NT;
-  const size_t lds = ((size_t)a.P * (a.P + 1) / 2 + 3 * PP + 8) * sizeof(double);
+  const size_t lds = ((size_t)a.P * (a.P + 1) / 2 + 3 * PP + 8 + 256) * sizeof(double);
   switch (a.NT) {
     case 1: return launch_solve_t<1>(a, K, lds, s);
     case 2: return launch_solve_t<2>(a, K, lds, s);

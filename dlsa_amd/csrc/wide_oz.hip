@@ -62,7 +62,8 @@ __global__ __launch_bounds__(256) void wide_oz_scale_kernel(const WideArgs a, co
     }
     const double bound = __hiloint2double((int)(m & 0x7FFFFFFFu), (int)0xFFFFFFFFu);
     int e = __builtin_amdgcn_frexp_exp(bound);
-    o.E[(int64_t)g * PP + f] = min(max(e, ozk::EMIN), ozk::EMAX);
+    // EMAX + 1 marks |z| >= 2^EMAX (digits would wrap): the tile kernel writes NaN
+    o.E[(int64_t)g * PP + f] = min(max(e, ozk::EMIN), ozk::EMAX + 1);
   }
 }
 
@@ -88,7 +89,7 @@ __global__ __launch_bounds__(256) void wide_oz_digits_kernel(const WideArgs a, c
   for (int m = 0; m < MB; ++m) {
     const int f = lane + 64 * m, j = f - ic;
     const bool inb = j >= 0 && j < p;
-    const double sc = __builtin_amdgcn_ldexp(1.0, 38 - o.E[(int64_t)g * PP + f]);
+    const double sc = __builtin_amdgcn_ldexp(1.0, 38 - min(o.E[(int64_t)g * PP + f], ozk::EMAX));
     double cen = 0.0, isc = 1.0;
     if constexpr (STD) {
       if (inb) {
@@ -262,7 +263,10 @@ __global__ __launch_bounds__(512, 1) void wide_oz_gram_kernel(const WideArgs a, 
       for (int r = 0; r < 4; ++r) {
         const int il = 64 * qi + 16 * si + 4 * gq + r;
         const double v = ozk::level_value(acc[si][u], r);
-        G[il * kOzGT + jl] = __builtin_amdgcn_ldexp(v, E[kOzGT * I + il] + ej - 12);
+        const int ei = E[kOzGT * I + il];
+        G[il * kOzGT + jl] = (ozk::digit_overflow(ei) || ozk::digit_overflow(ej))
+                                 ? __builtin_nan("")
+                                 : __builtin_amdgcn_ldexp(v, ei + ej - 12);
       }
   }
 }

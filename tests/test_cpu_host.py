@@ -92,6 +92,28 @@ def test_native_lars_vs_oracle_random(seed, intercept, typ):
     assert np.allclose(r["beta0"], o["beta0"], rtol=1e-10, atol=1e-10)
 
 
+@pytest.mark.parametrize("seed", [9, 13, 37])
+def test_native_lars_drop_heavy_vs_oracle(seed):
+    """LASSO paths with 5-7 drops (low-rank correlated designs): after each
+    drop the kept columns are renumbered in active order, so the path after a
+    drop follows the oracle (lsa.py:90-212) as closely as before one."""
+    from dlsa_amd.lsa import lars_lsa
+
+    rs = np.random.RandomState(seed)
+    m = 40
+    Z = rs.randn(3 * m, 8)
+    A = Z @ rs.randn(8, m) + 0.3 * rs.randn(3 * m, m)
+    S = A.T @ A
+    b = rs.randn(m)
+    o = O.lars_lsa(S, b, False, 1000, type="lasso")
+    nz = np.abs(o["beta"]) > 0
+    assert int((nz[:-1] & ~nz[1:]).sum()) >= 5
+    r = lars_lsa(S, b, False, 1000, type="lasso")
+    assert r["beta"].shape == o["beta"].shape
+    assert np.abs(r["beta"] - o["beta"]).max() < 1e-10 * max(1.0, np.abs(o["beta"]).max())
+    assert np.allclose(r["BIC"], o["BIC"], rtol=1e-10, atol=1e-8)
+
+
 def test_native_lars_vs_oracle_config5_size():
     """LASSO path at the config-5 width class (m = 400, 401 knots): the native
     path (permuted-Sigma equiangular products, transposed-R back solve) against

@@ -402,3 +402,19 @@ def test_wide_ozaki_digit_records_stay_in_bounds(torch_cuda, M, p, rows):
     th, S, st, ws = _abi_fit(torch, X, y, off, p, need, guard=1 << 20, rows_per_chunk=rows)
     assert st["passes_oz"] >= 1
     assert (ws[need:].cpu().numpy() == 0xA5).all()
+
+
+@pytest.mark.parametrize("kind", ["separable", "outlier"])
+def test_ozaki_polish_pass_per_entry(torch_cuda, M, monkeypatch, kind):
+    """A budget that runs out (max_iter = 4) on heavy designs: the polish
+    pass publishes Sig_inv at the returned theta on the int8 cores, with
+    digit exponents from records taken at other iterates (the growth bound
+    exp(|dtheta|_1 max|x| / 2) is then the only margin).  Per entry within
+    1e-10 of the fp64-MFMA pass at the same iterate (advisor finding, r4)."""
+    X, y = heavy_design(kind, 24000, seed=4)
+    off = np.array([0, 7000, 15000, 24000])
+    oz, f64 = _pair(M, monkeypatch, X, y, off, max_iter=4, rows_per_chunk=2048)
+    assert oz.stats["polish_partitions"] >= 1, oz.stats
+    assert oz.stats["passes_oz"] >= 1, oz.stats
+    assert _rel(oz.theta.cpu(), f64.theta.cpu()) < 1e-10
+    assert _elem(oz.sig_inv.cpu(), f64.sig_inv.cpu()) < 1e-10

@@ -230,3 +230,25 @@ def test_categorical_inf_fails_only_its_partition(torch_cuda, M):
         from dlsa_amd.dlsa import reduce_partitions_device
         buf = reduce_partitions_device(fit).cpu().numpy()
     assert np.isfinite(buf).all()
+
+
+@pytest.mark.parametrize("p", [8, 200])
+def test_huge_magnitude_fails_only_its_partition(torch_cuda, M, p):
+    """A value of 2^1010 in partition 1 (beyond the int8 digit grid's EMAX:
+    its digits would wrap to a finite, wrong Gram): partition 1 must end in a
+    failure status -- never status ok with a finite Sig_inv -- and the other
+    partitions match the oracle (fused P <= 192 and wide P > 192 paths)."""
+    rng = np.random.default_rng(5 + p)
+    n_k, K = 3000, 3
+    X = rng.normal(size=(n_k * K, p)) * 0.3
+    y = (rng.random(n_k * K) < _expit(X @ (rng.normal(size=p) * 0.2))).astype(np.float64)
+    X[n_k + 77, 2] = 2.0 ** 1010
+    off = np.arange(K + 1, dtype=np.int64) * n_k
+    fit = M.logistic_model_batched(X, y, off)
+    st = fit.status.cpu().numpy()
+    assert st[1] != 0, st
+    for k in (0, 2):
+        o = O.logistic_fit(X[off[k]:off[k + 1]], y[off[k]:off[k + 1]])
+        assert st[k] == 0, st
+        assert _rel(fit.theta[k].cpu(), o["coef"]) < REL
+        assert _rel(fit.sig_inv[k].cpu(), o["Sig_inv"]) < REL

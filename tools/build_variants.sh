@@ -41,6 +41,7 @@ for v in "$@"; do
     ozs1) D=DLSA_OZ_SCHED=1 ;;
     ozs2) D=DLSA_OZ_SCHED=2 ;;
     oz6) D=DLSA_OZ_LEVELS=6 ;;
+    cmabl) D=DLSA_CM_ABLATE=1 ;;
     nt) D=DLSA_X_DMA_AUX=2 ;;
     dma0) D=DLSA_X_DMA_AUX=0 ;;
     sc1) D=DLSA_X_DMA_AUX=1 ;;
@@ -50,6 +51,7 @@ for v in "$@"; do
   case $v in
     oz*|ozs*) ONLY='["irls_oz.hip", "irls_oz_g2.hip"]' ;;
     solve*) ONLY='["newton_solve.hip"]' ;;
+    cmabl) ONLY='["irls_coop_g1.hip", "irls_coop_g2.hip", "irls_coop_g3.hip", "irls_coop_g4.hip", "irls_coop_g5.hip", "irls_coop_g6.hip"]' ;;
     ols*|wslot3) ONLY='["irls_wave.hip", "irls_wave_g2.hip"]' ;;
   esac
   python -c "from dlsa_amd.build import build; print(build(force=True, out='var/libdlsa_hip_$v.so', defines='$D'.replace('-D', '').split(), only=$ONLY))"
