@@ -72,13 +72,16 @@ struct Plan {
 // (profiles/r02ap_c2_chunk_ab.txt, r02ar_c2_chunk_ab.txt); at the
 // strong-scaling share of config 2 (n = 1.25e7 per GPU, 1525 rows per chunk
 // by the old rule) 3072 / 6144-row chunks fit 12.8 / 12.7 ms against 13.5 ms
-// (fewer per-chunk prologues and partial tiles; r02am).
+// (fewer per-chunk prologues and partial tiles; r02am).  Round 5 (current
+// kernels, r05j, alternated): at that share 4096 / 6144 / 8192 / 12288 rows
+// per chunk fit 11.10-11.28 / 10.70-10.73 / 10.85-10.97 / 10.71-10.81 ms, so the
+// floor is 6144 rows (2048 chunks there; config 2 itself is unchanged).
 static int auto_rows_per_chunk(int64_t n_total) {
   if (const char* e = env_knob("DLSA_ROWS_PER_CHUNK")) return std::max(64, atoi(e));
   // rounded up to a multiple of 1024: equal partitions then split into whole
   // chunks (config 2: 16384 rows, 6 per partition) instead of a ragged extra one
   int64_t r = (n_total / 6144 + 1023) / 1024 * 1024;
-  r = std::max<int64_t>(4096, std::min<int64_t>(r, 131072));
+  r = std::max<int64_t>(6144, std::min<int64_t>(r, 131072));
   return (int)r;
 }
 

@@ -875,11 +875,20 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
                                  a.zcolmax[(int64_t)chunk * PMAX + tid], growth,
                                  FAM == FAMILY_LOGISTIC);
     ex[tid] = min(e, ozk::EMAX);
-    e_ovf = ozk::digit_overflow(e);
+    if (wid == 0) {  // wave 0 (whose tid 0 publishes slab_ll) also checks wave 1's features
+      e_ovf = ozk::digit_overflow(e);
+      if (tid + 64 < PMAX)
+        e_ovf = e_ovf || ozk::digit_overflow(digit_exponent(
+                             a.colmax[(int64_t)chunk * PMAX + tid + 64],
+                             a.zcolmax[(int64_t)chunk * PMAX + tid + 64], growth,
+                             FAM == FAMILY_LOGISTIC));
+    }
   }
+  // (no __syncthreads_or: its __shared__ word would push the LDS past 160 KB)
+  const bool chunk_ovf = wid == 0 && __ballot(e_ovf) != 0;
   // (the ring needs no zeroing: past-the-chunk rows are zeroed in registers
   // and nothing reads a slot's bytes that the DMA did not write)
-  const bool chunk_ovf = __syncthreads_or(e_ovf) != 0;
+  __syncthreads();
 
   auto slot_x = [&](int blk) -> char* {
     const uintptr_t start = (uintptr_t)(a.X + (row0 + (int64_t)blk * RB) * p);

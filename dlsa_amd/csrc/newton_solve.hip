@@ -1,4 +1,4 @@
-// Per-partition Newton update (one 256-thread workgroup per partition).
+// Per-partition Newton update (one 1024-thread workgroup per partition).
 //
 // Replaces the outer Newton step of sklearn's newton-cg solve inside
 // dlsa/models.py:110-113 (the reference solves H d = g iteratively by CG with
@@ -32,6 +32,17 @@
 
 namespace dlsa {
 
+// Threads per partition (NTHR): 1024 when K <= 256 -- one partition per CU,
+// so the trailing updates (the bulk of the Cholesky at P >= 100) spread over
+// 16 waves instead of 4 and the assembly holds T / 4 tiles per thread (configs
+// 3, 5-share and the N = 8 share of config 2: K = 120-128); 256 above, where
+// three partitions share a CU (config 2, K = 1024: the LDS of the packed
+// triangle allows 3).  The diagonal blocks and triangular solves stay on wave 0.
+constexpr int kMaxSolveWaves = 16;
+constexpr int kRedFlag = kMaxSolveWaves, kRedSink = kMaxSolveWaves + 1,
+              kRedLL = kMaxSolveWaves + 2, kRedZero = kMaxSolveWaves + 3;
+constexpr int kRedSize = kMaxSolveWaves + 4;
+
 __device__ __forceinline__ double block_max(double v, double* red) {
   for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
   const int w = threadIdx.x >> 6;
@@ -61,8 +72,9 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
 // Packed lower triangle: element (i, j), i >= j, at i (i + 1) / 2 + j.
 __device__ __forceinline__ int tri(int i, int j) { return i * (i + 1) / 2 + j; }
 
-template <int NT>
-__global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
+template <int NT, int NTHR>
+__global__ __launch_bounds__(NTHR) void newton_solve_kernel(const SolveArgs a) {
+  constexpr int kSolveThreads = NTHR, kSolveWaves = NTHR / 64;
   extern __shared__ __attribute__((aligned(16))) double sm[];
   constexpr int T = NT * (NT + 1) / 2;
   constexpr int PP = 16 * NT;
@@ -81,7 +93,7 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
   double* g = H + P * (P + 1) / 2;   // PP
   double* z = g + PP;                // PP
   double* invd = z + PP;             // PP: 1 / L_jj
-  double* red = invd + PP;           // 8: [0..3] block reductions, [5] flag, [6] store sink, [7] ll
+  double* red = invd + PP;           // kRedSize: [0, kSolveWaves) per-wave values, flag, sink, ll
 
   // chunk partials were summed into the partition's first chunk by
   // partials_sum_kernel (fixed chunk order)
@@ -101,28 +113,36 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
 #endif
   SOLVE_MARK(0)
 
-  // 1. assemble: thread tid owns element (tile t, position tid) of every
-  //    tile.  Only the
-  //    lower triangle is kept (diagonal tiles hold (w x_i) x_j and (w x_j) x_i,
-  //    equal up to the last bit): Sig_inv comes out exactly symmetric.
+  // 1. assemble: thread tid owns position tid % 256 of the tiles
+  //    t = tid / 256 + 4 u (the partition's partials were summed into its first
+  //    chunk by partials_sum_kernel).  Only the lower triangle is kept
+  //    (diagonal tiles hold (w x_i) x_j and (w x_j) x_i, equal up to the last
+  //    bit): Sig_inv comes out exactly symmetric.
   {
-    double acc[T];
-#pragma unroll
-    for (int t = 0; t < T; ++t) acc[t] = 0.0;
+    constexpr int G = kSolveThreads / 256;
+    constexpr int TG = (T + G - 1) / G;
+    const int pos = tid & 255, grp = tid >> 8;
+    const int r = pos >> 4, q = pos & 15;
     for (int c = cb; c < ce; ++c) {
-      const double* src = a.slab_H + (int64_t)c * T * 256 + tid;
+      const double* src = a.slab_H + (int64_t)c * T * 256 + pos;
+      constexpr int UB = TG < 8 ? TG : 8;  // tiles loaded together (unconditional loads)
 #pragma unroll
-      for (int t = 0; t < T; ++t) acc[t] += src[t * 256];
-    }
-    const int r = tid >> 4, q = tid & 15;
+      for (int u0 = 0; u0 < TG; u0 += UB) {
+        double v[UB];
 #pragma unroll
-    for (int I = 0; I < NT; ++I)
+        for (int u = 0; u < UB; ++u) v[u] = src[min(grp + G * (u0 + u), T - 1) * 256];
 #pragma unroll
-      for (int J = 0; J <= I; ++J) {
-        const int t = I * (I + 1) / 2 + J;
-        const int gi = 16 * I + r, gj = 16 * J + q;
-        if (gi < P && gi >= gj) H[tri(gi, gj)] = acc[t];
+        for (int u = 0; u < UB; ++u) {
+          const int t = grp + G * (u0 + u);
+          if (u0 + u < TG && t < T) {
+            int I = 0;
+            while ((I + 1) * (I + 2) / 2 <= t) ++I;
+            const int gi = 16 * I + r, gj = 16 * (t - I * (I + 1) / 2) + q;
+            if (gi < P && gi >= gj) H[tri(gi, gj)] = v[u];
+          }
+        }
       }
+    }
   }
   if (tid < PP) {
     double s = 0.0;
@@ -133,17 +153,17 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
     double s = 0.0;
     for (int c = cb + lane; c < ce; c += 64) s += a.slab_ll[c];
     s = wave_sum(s);
-    if (lane == 0) red[7] = s;
+    if (lane == 0) red[kRedLL] = s;
   }
   __syncthreads();
-  const double ll = red[7];
+  const double ll = red[kRedLL];
   const int it = a.iters[k];
   double* th = a.theta + (int64_t)k * P;
 
   // a warm-start level that fails (separation, too few rows) only restarts
   // the partition from theta = 0 on the next level
   auto level_fail = [&]() {
-    for (int f = tid; f < P; f += 256) th[f] = 0.0;
+    for (int f = tid; f < P; f += kSolveThreads) th[f] = 0.0;
     if (tid == 0) {
       a.phase[k] = PHASE_LEVEL_DONE;
       a.iters[k] = it + 1;
@@ -167,7 +187,7 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
     const double sc = ldexp(1.0, -bt);
     const double* tp = a.theta_prev + (int64_t)k * P;
     const double* dp = a.delta_prev + (int64_t)k * P;
-    for (int f = tid; f < P; f += 256) th[f] = tp[f] + sc * dp[f];
+    for (int f = tid; f < P; f += kSolveThreads) th[f] = tp[f] + sc * dp[f];
     if (tid == 0) {
       a.backtracks[k] = bt;
       a.iters[k] = it + 1;
@@ -185,7 +205,7 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
   // 3. publish the information matrix at the evaluation point --------------
   if (!a.subsample) {
     double* S = a.sig_inv + (int64_t)k * P * P;
-    for (int e = tid; e < P * P; e += 256) {
+    for (int e = tid; e < P * P; e += kSolveThreads) {
       const int i = e / P, j = e - i * P;
       S[e] = H[i >= j ? tri(i, j) : tri(j, i)];
     }
@@ -205,7 +225,10 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
   //    Three barriers per 16 columns (was one per column with a serial
   //    per-thread row update).
   SOLVE_MARK(2)
-  if (tid == 0) red[5] = 0.0;
+  if (tid == 0) {
+    red[kRedFlag] = 0.0;
+    red[kRedZero] = 0.0;  // read by the triangular solves off the triangle
+  }
   __syncthreads();
   bool ok = true;
   for (int b = 0; b < NT; ++b) {
@@ -237,8 +260,13 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
         if (kk < nb) {  // wave-uniform
           const double dkk = readlane_f64(av[kk], kk);
           good = good && dkk > 0.0 && isfinite(dkk);
-          const double lkk = sqrt(dkk);
-          const double il = 1.0 / lkk;
+          // 1 / sqrt(d) by v_rsq_f64 + two Newton steps (~1 ulp), L_kk = d / sqrt(d):
+          // the serial chain of the block is 16 of these (IEEE sqrt + division:
+          // ~2x the dependent latency)
+          double il = __builtin_amdgcn_rsq(dkk);
+#pragma unroll
+          for (int nr = 0; nr < 2; ++nr) il = fma(il, fma(-0.5 * dkk * il, il, 0.5), il);
+          const double lkk = dkk * il;
           if (lv == kk) ild = il;
           av[kk] = (i > kk) ? av[kk] * il : (i == kk ? lkk : av[kk]);
 #pragma unroll
@@ -250,16 +278,16 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
         }
       }
 #pragma unroll
-      for (int j = 0; j < 16; ++j) *((act && j <= i) ? H + tri(ri, c0 + j) : red + 6) = av[j];
+      for (int j = 0; j < 16; ++j) *((act && j <= i) ? H + tri(ri, c0 + j) : red + kRedSink) = av[j];
       if (lv < 16) {
 #pragma unroll
         for (int j = 0; j < 16; ++j) dblk[16 * lv + j] = j < i ? av[j] : (j == i ? ild : 0.0);
       }
-      if (lv == 0 && !good) red[5] = 1.0;
+      if (lv == 0 && !good) red[kRedFlag] = 1.0;
     }
     __syncthreads();
     SOLVE_PAN(1)
-    if (red[5] != 0.0) {  // block-uniform
+    if (red[kRedFlag] != 0.0) {  // block-uniform
       ok = false;
       break;
     }
@@ -284,7 +312,7 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
       const int m = NT - b - 1;  // tile rows below the panel
       const int ntile = m * (m + 1) / 2;
       const int fl = lv & 15, q = lv >> 4;
-      for (int t = wid; t < ntile; t += 4) {  // wave-uniform
+      for (int t = wid; t < ntile; t += kSolveWaves) {  // wave-uniform
         int I = 0;
         while ((I + 1) * (I + 2) / 2 <= t) ++I;
         const int J = t - I * (I + 1) / 2;
@@ -312,7 +340,7 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
           acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-x_a, x_b, acc, 0, 0, 0);
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) *(adr[r] >= 0 ? H + adr[r] : red + 6) = acc[r];
+        for (int r = 0; r < 4; ++r) *(adr[r] >= 0 ? H + adr[r] : red + kRedSink) = acc[r];
       }
     }
     __syncthreads();
@@ -350,15 +378,18 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
   if (wid == 0) {
     constexpr int U = 4;
     double zr[R], ir[R];
+    const double* hrow[R];  // row base of lane row i (clamped to P - 1): L[i][j] = hrow[j]
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int i = lane + 64 * r;
       zr[r] = i < P ? g[i] : 0.0;
       ir[r] = i < P ? invd[i] : 0.0;
+      hrow[r] = H + tri(min(i, P - 1), 0);
     }
     for (int j0 = 0; j0 < P; j0 += U) {
       // lane index re-defined per step group (no hoisted lane masks to spill);
-      // unconditional in-triangle loads (row clamped to [j, P - 1]) + selects
+      // unconditional loads (row base + j stays inside the allocation; the
+      // entries off the strict lower triangle are selected away)
       int lv = lane;
       asm volatile("" : "+v"(lv));
       double hv[U][R];
@@ -366,9 +397,10 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
       for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-          const int i = lv + 64 * r, j = min(j0 + u, P - 1);
-          const double h = H[tri(max(min(i, P - 1), j), j)];
-          hv[u][r] = (j0 + u < P && i > j && i < P) ? h : 0.0;
+          const int i = lv + 64 * r, j = j0 + u;
+          // off the strict lower triangle: the zero word (an address select,
+          // one v_cndmask instead of two on the loaded value)
+          hv[u][r] = *((j < P && i > j && i < P) ? hrow[r] + j : red + kRedZero);
         }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -396,9 +428,8 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
       for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-          const int i = lv + 64 * r, j = max(j0 - u, 0);
-          const double h = H[tri(j, 0) + min(i, j)];
-          hv[u][r] = (j0 - u >= 0 && i < j) ? h : 0.0;
+          const int i = lv + 64 * r, j = j0 - u;
+          hv[u][r] = *((j >= 0 && i < j) ? H + tri(j, 0) + i : red + kRedZero);
         }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -435,7 +466,7 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
   double dm = 0.0, tm = 0.0, tg = 0.0;
   double* tp = a.theta_prev + (int64_t)k * P;
   double* dp = a.delta_prev + (int64_t)k * P;
-  for (int f = tid; f < P; f += 256) {
+  for (int f = tid; f < P; f += kSolveThreads) {
     const double d = z[f];
     const double t0 = th[f];
     const double t1 = t0 + d;
@@ -452,7 +483,7 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
     // keep the last finite iterate (each thread restores the entries it
     // wrote): the status reports the failure and the combine step excludes
     // the partition
-    for (int f = tid; f < P; f += 256) th[f] = tp[f];
+    for (int f = tid; f < P; f += kSolveThreads) th[f] = tp[f];
   }
   if (a.family == FAMILY_GAUSSIAN) {
     // OLS: theta was 0, one Newton step is the closed form (X^T X)^-1 X^T y;
@@ -462,7 +493,10 @@ __global__ __launch_bounds__(256) void newton_solve_kernel(const SolveArgs a) {
     if (lane == 0) red[wid] = tg;
     __syncthreads();
     if (tid == 0) {
-      a.loglik[k] = -2.0 * ll - (red[0] + red[1] + red[2] + red[3]);
+      double tgs = 0.0;
+#pragma unroll
+      for (int w = 0; w < kSolveWaves; ++w) tgs += red[w];
+      a.loglik[k] = -2.0 * ll - tgs;
       a.iters[k] = it + 1;
       a.status[k] = isfinite(dm) ? DLSA_STATUS_OK : DLSA_STATUS_NONFINITE;
       a.phase[k] = PHASE_DONE;
@@ -562,19 +596,21 @@ __global__ __launch_bounds__(256) void partials_sum_kernel(const SolveArgs a, in
 
 template <int NT>
 static hipError_t launch_solve_t(const SolveArgs& a, int K, size_t lds, hipStream_t s) {
+  const bool wide = K <= 256;
+  auto kern = wide ? newton_solve_kernel<NT, 1024> : newton_solve_kernel<NT, 256>;
   {
-    hipError_t e = ensure_max_lds((const void*)newton_solve_kernel<NT>, 160 * 1024);
+    hipError_t e = ensure_max_lds((const void*)kern, 160 * 1024);
     if (e != hipSuccess) return e;
   }
   constexpr int T = NT * (NT + 1) / 2;
   hipLaunchKernelGGL(partials_sum_kernel, dim3((T + 1 + 3) / 4, K), dim3(256), 0, s, a, T, 16 * NT);
-  hipLaunchKernelGGL(newton_solve_kernel<NT>, dim3(K), dim3(256), lds, s, a);
+  hipLaunchKernelGGL(kern, dim3(K), dim3(wide ? 1024 : 256), lds, s, a);
   return hipGetLastError();
 }
 
 hipError_t launch_newton_solve(const SolveArgs& a, int K, hipStream_t s) {
   const int PP = 16 * a.NT;
-  const size_t lds = ((size_t)a.P * (a.P + 1) / 2 + 3 * PP + 8 + 256) * sizeof(double);
+  const size_t lds = ((size_t)a.P * (a.P + 1) / 2 + 3 * PP + kRedSize + 256) * sizeof(double);
   switch (a.NT) {
     case 1: return launch_solve_t<1>(a, K, lds, s);
     case 2: return launch_solve_t<2>(a, K, lds, s);

@@ -411,7 +411,7 @@ def test_ozaki_polish_pass_per_entry(torch_cuda, M, monkeypatch, kind):
     digit exponents from records taken at other iterates (the growth bound
     exp(|dtheta|_1 max|x| / 2) is then the only margin).  Per entry within
     1e-10 of the fp64-MFMA pass at the same iterate (advisor finding, r4)."""
-    X, y = heavy_design(kind, 24000, seed=4)
+    X, y = heavy_design(kind, 24000, seed=4, p_extra=6)  # P = 13: the in-place images fit
     off = np.array([0, 7000, 15000, 24000])
     oz, f64 = _pair(M, monkeypatch, X, y, off, max_iter=4, rows_per_chunk=2048)
     assert oz.stats["polish_partitions"] >= 1, oz.stats
