@@ -1027,6 +1027,13 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
   double* d_threc = (double*)at(L.off_threc);
   bool colmax_ready = false;
   bool near_switch = false;  // counters[3] of the last solve
+  // per partition: the last approximate pass that processed it recorded max |z|
+  // (so its exact pass starts from a record one small step away); an exact
+  // pass with any partition lacking one runs on the fp64 MFMA instead: without
+  // a fresh record the digit exponents fall back to max |x| / 2, which a
+  // column with large |x| at w ~ 0 (an outlier row) turns into ~1e-5 per-entry
+  // errors (tests/test_gpu_ozaki.py::test_ozaki_polish_pass_per_entry)
+  std::vector<char> zfresh((size_t)K, 0);
   // DLSA_OZ_ZREC=0 (A/B only): no max |z| records, every exponent from max |x| / 2
   const bool zrec = !(env_knob("DLSA_OZ_ZREC") && atoi(env_knob("DLSA_OZ_ZREC")) == 0);
   if (use_oz) {
@@ -1045,7 +1052,10 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
     const int prec = f64 ? PREC_F64 : (ph == PHASE_F32X ? PREC_F32 : approx_prec);
     pa.want_phase = ph;
     const bool wave = f64 && q.NT <= kWaveMaxNT;
-    const bool oz = wave && use_oz && colmax_ready && full;
+    bool fresh = true;
+    if (f64)
+      for (int k = 0; k < K; ++k) fresh = fresh && (hph[k] != PHASE_F64 || zfresh[k]);
+    const bool oz = wave && use_oz && colmax_ready && full && fresh;
     // digit-scale records of a full-data bf16 pass: max |x| on the first,
     // max |z| near the switch
     const bool rec_x = use_oz && full && ph == PHASE_F32 && !colmax_ready;
@@ -1064,6 +1074,9 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
       return launch_irls_coop(pc, q.NT, prec, standardize, family, q.n_chunks, stream);
     });
     if (rec_x) colmax_ready = true;
+    if (!f64)  // this pass's partitions moved on from their records unless it took one
+      for (int k = 0; k < K; ++k)
+        if (hph[k] == ph) zfresh[k] = rec_z;
     if (oz) g_stats.passes_oz++;
     if (f64) {
       g_stats.passes_fp64++;
@@ -1123,6 +1136,10 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
   // (models.py:114,130 evaluate the weights at the coef sklearn stopped at)
   if (family == FAMILY_LOGISTIC && running_total(n_running) > 0 && pl.n_chunks > 0) {
     // (the final level's plan, pl, is on the device: it was the last uploaded)
+    // a partition stopped in an approximate phase took a full step after its
+    // last record: its polish pass cannot use that record
+    for (int k = 0; k < K; ++k)
+      if (h_phase[k] != PHASE_F64) zfresh[k] = 0;
     DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
     DLSA_HIP_TRY(launch_polish_mark(K, d_phase, status, d_cnt, stream));
     DLSA_HIP_TRY(hipMemcpyAsync(h_phase, d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));

@@ -407,14 +407,17 @@ def test_wide_ozaki_digit_records_stay_in_bounds(torch_cuda, M, p, rows):
 @pytest.mark.parametrize("kind", ["separable", "outlier"])
 def test_ozaki_polish_pass_per_entry(torch_cuda, M, monkeypatch, kind):
     """A budget that runs out (max_iter = 4) on heavy designs: the polish
-    pass publishes Sig_inv at the returned theta on the int8 cores, with
-    digit exponents from records taken at other iterates (the growth bound
-    exp(|dtheta|_1 max|x| / 2) is then the only margin).  Per entry within
-    1e-10 of the fp64-MFMA pass at the same iterate (advisor finding, r4)."""
+    pass publishes Sig_inv at the returned theta.  A partition stopped in an
+    approximate phase took a full Newton step after its last max |z| record,
+    so the growth bound exp(|dtheta|_1 max|x| / 2) would be the only margin
+    (advisor finding, r4) -- on the outlier design that left 8e-5 per entry
+    (round-5 run r05k).  The exact pass therefore runs on the int8 cores only
+    when every partition in it has a record from its last approximate pass
+    (capi.hip zfresh), else on the fp64 MFMA.  Per entry within 1e-10 of the
+    fp64-MFMA pass at the same iterate."""
     X, y = heavy_design(kind, 24000, seed=4, p_extra=6)  # P = 13: the in-place images fit
     off = np.array([0, 7000, 15000, 24000])
     oz, f64 = _pair(M, monkeypatch, X, y, off, max_iter=4, rows_per_chunk=2048)
     assert oz.stats["polish_partitions"] >= 1, oz.stats
-    assert oz.stats["passes_oz"] >= 1, oz.stats
     assert _rel(oz.theta.cpu(), f64.theta.cpu()) < 1e-10
     assert _elem(oz.sig_inv.cpu(), f64.sig_inv.cpu()) < 1e-10
