@@ -470,7 +470,10 @@ def main():
         n32, n64 = tot("passes_fp32"), tot("passes_fp64")
         rows32, rows64 = tot("rows_fp32"), tot("rows_fp64")
         n_oz = tot("passes_oz")
+        ols_stream = family == "ols" and NT <= 4  # capi.hip: ols_stream_applies
         exact = (f"irls_oz_kernel<NT={NT}> (exact pass, int8-MFMA digit slices)" if n_oz
+                 else f"ols_stream_kernel<NT={NT}> (X streamed into the fp64 MFMA operands)"
+                 if ols_stream
                  else f"irls_wave_kernel<NT={NT},fp64> (per-wave exact pass)" if NT <= 8
                  else f"irls_coop_kernel<NT={NT},fp64 Hessian>")
         if n32:
@@ -507,7 +510,7 @@ def main():
             # config 4 is HBM-bound (65 GB vs 0.54 TF per GPU)
             roof = hbm_roof(exact + " (OLS: X^T X, X^T y in one pass)", ms64, n64, rows64)
             roof["mfma_issued_frac"] = kern[exact].get("mfma_frac")
-            pmc_key = "irls_wave<ols>"
+            pmc_key = "ols_stream" if ols_stream else "irls_wave<ols>"
         elif n_oz:  # the int8 exact pass streams X once: HBM-bound
             roof = hbm_roof(exact, ms64, n64, rows64)
             roof["int8_mfma_frac"] = kern[exact]["int8_mfma_frac"]

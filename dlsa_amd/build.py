@@ -20,7 +20,7 @@ CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libdlsa_hip.so")
 SOURCES = (["irls_coop.hip"] + [f"irls_coop_g{i}.hip" for i in range(1, 7)] +
            ["irls_wave.hip", "irls_wave_g2.hip", "irls_oz.hip", "irls_oz_g2.hip"] +
-           ["wide_pass.hip", "wide_oz.hip", "cat_pass.hip", "partition_rows.hip", "moments.hip", "eval_pass.hip", "newton_solve.hip", "aux_kernels.hip", "capi.hip", "lars_host.cpp"])
+           ["wide_pass.hip", "wide_oz.hip", "cat_pass.hip", "partition_rows.hip", "moments.hip", "ols_stream.hip", "eval_pass.hip", "newton_solve.hip", "aux_kernels.hip", "capi.hip", "lars_host.cpp"])
 HEADERS = ["dlsa_internal.hpp", "irls_coop_impl.hpp", "irls_wave_impl.hpp", "irls_oz_impl.hpp", os.path.join("..", "..", "include", "dlsa_hip.h")]
 ARCH = os.environ.get("DLSA_OFFLOAD_ARCH", "gfx950")
 

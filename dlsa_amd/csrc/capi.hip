@@ -1070,6 +1070,9 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
       pc.zcolmax = (oz || rec_z) ? d_zcolmax : nullptr;
       pc.theta_rec = d_threc;
       if (oz) return launch_irls_oz(pc, q.NT, standardize, family, q.n_chunks, stream);
+      // OLS (one pass at theta = 0): X streamed into registers, no LDS ring
+      if (f64 && family == FAMILY_GAUSSIAN && ols_stream_applies(q.NT))
+        return launch_ols_stream(pc, q.NT, standardize, q.n_chunks, stream);
       if (wave) return launch_irls_wave(pc, q.NT, standardize, family, q.n_chunks, stream);
       return launch_irls_coop(pc, q.NT, prec, standardize, family, q.n_chunks, stream);
     });

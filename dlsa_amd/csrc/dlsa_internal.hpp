@@ -335,6 +335,11 @@ hipError_t launch_irls_oz(const PassArgs& a, int NT, bool standardize, int famil
 bool oz_applies(int NT, int p);  // NT <= kOzMaxNT, image and 6-slot ring fit
 constexpr int kOzMaxRows = 32767;
 constexpr int kOzMaxNT = 7;
+// OLS pass at theta = 0 streaming X into the MFMA operand registers
+// (ols_stream.hip), P <= 64
+bool ols_stream_applies(int NT);
+hipError_t launch_ols_stream(const PassArgs& a, int NT, bool standardize, int n_chunks,
+                             hipStream_t s);
 hipError_t launch_irls_coop(const PassArgs& a, int NT, int prec, bool standardize, int family,
                             int n_chunks, hipStream_t s);
 int coop_slot_bytes(int NT, int p);

@@ -80,8 +80,12 @@ extern "C" {
 /* Arithmetic of the exact pass in the MIXED modes.
  * DLSA_EXACT_AUTO: X^T W X from int8 digit slices on the int8 matrix cores
  *   (the Ozaki scheme) wherever it applies -- P <= 112 with chunks of at most
- *   32767 rows, and P > DLSA_MAX_P_FUSED when the workspace holds the digit
- *   records -- otherwise fp64 MFMA.  z = sqrt(w) x is rounded to a 38-bit
+ *   32767 rows, every partition of the pass carrying a max |z| record from
+ *   its last approximate pass (a partition stopped by max_iter in an
+ *   approximate phase does not), and P > DLSA_MAX_P_FUSED when the workspace
+ *   holds the digit records -- otherwise fp64 MFMA.  A chunk whose bound on
+ *   |z| passes 2^1009 fails its partition (non-finite) instead of wrapping
+ *   its digits.  z = sqrt(w) x is rounded to a 38-bit
  *   fixed-point grid below 2^E_f per chunk (or row group) and feature, the
  *   digit products are summed exactly in int32 and the levels below 2^-40 of
  *   the leading product are dropped: every entry of Sig_inv is within about

@@ -29,7 +29,7 @@ rows = []
 for f in sorted(glob.glob(os.path.join(base, "**", "*counter_collection.csv"), recursive=True)):
     i = os.path.relpath(f, base).split(os.sep)[0]  # one counter group per run directory
     for r in csv.DictReader(open(f)):
-        if any(t in r["Kernel_Name"] for t in ("irls_", "wide_", "cat_", "part_")):
+        if any(t in r["Kernel_Name"] for t in ("irls_", "wide_", "cat_", "part_", "ols_")):
             rows.append({"pass": i, "dispatch": r["Dispatch_Id"],
                          "kernel": r["Kernel_Name"][:120], "grid": int(r["Grid_Size"]),
                          "counter": r["Counter_Name"], "value": float(r["Counter_Value"]),
