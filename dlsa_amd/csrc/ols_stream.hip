@@ -32,6 +32,17 @@ namespace {
 typedef double d4o __attribute__((ext_vector_type(4)));
 constexpr int kOlsWaves = 4;  // independent waves (chunks) per workgroup
 
+// Buffer resource over [base, base + bytes) with every word wave-uniform
+// (readfirstlane: the loads take it in SGPRs).  Loads past `bytes` return 0.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ols_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t b = (uint64_t)(uintptr_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+  const uint32_t nr = __builtin_amdgcn_readfirstlane(bytes);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, (int)nr,
+                                           0x00020000);
+}
+
 // FULL: no intercept and p = 16 NT (every lane's features are columns of X,
 // config 4): full row groups take their operands as loaded, no selects
 template <int NT, int KS, bool STD, bool FULL>
@@ -76,49 +87,51 @@ __global__ __launch_bounds__(64 * kOlsWaves) void ols_stream_kernel(const PassAr
   for (int c = 0; c < NT; ++c) gacc[c] = 0.0;
   double ll = 0.0;
 
-  const double* X = a.X + row0 * p;
-  const double* Y = a.y + row0;
+  // the chunk's rows as bounds-checked buffers: rows past the chunk read 0, so
+  // x, y (and with them the MFMA products, X^T y and y^2) vanish there without
+  // a select; the lane's byte offset in a row group is a constant VGPR and the
+  // group's row offset an SGPR -- no per-load address arithmetic
+  const __amdgpu_buffer_rsrc_t xr = ols_rsrc(a.X + row0 * p, (uint32_t)nrows * p * 8);
+  const __amdgpu_buffer_rsrc_t yr = ols_rsrc(a.y + row0, (uint32_t)nrows * 8);
+  int voff[NT];
+#pragma unroll
+  for (int c = 0; c < NT; ++c) voff[c] = (q * p + col[c]) * 8;
   // one group of KS k-steps (4 rows each) from row r0.  The fp64 MFMAs bound
   // this pass (10 x ~70 cycles per 4 rows at P = 64) and fp64 VALU work never
-  // overlaps them, so the per-value work is one select (FULL: every lane's
-  // feature is a column of X; rows past the chunk -> 0).  (A separate
-  // select-free body for whole groups made the compiler copy the T x 4
-  // accumulators AGPR <-> VGPR every group.)
+  // overlaps them: FULL groups (every lane's feature a column of X) feed the
+  // loaded values to the MFMAs as they are; otherwise one select per value
+  // (padding features, the intercept column, rows past the chunk).
   for (int r0 = 0; r0 < nrows; r0 += 4 * KS) {
     double xv[KS][NT], yv[KS];
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      const int rr = min(r0 + 4 * s + q, nrows - 1);
-      const double* xr = X + (int64_t)rr * p;
+      const int so = __builtin_amdgcn_readfirstlane((r0 + 4 * s) * p * 8);
 #pragma unroll
-      for (int c = 0; c < NT; ++c) xv[s][c] = xr[col[c]];
-      yv[s] = Y[rr];
+      for (int c = 0; c < NT; ++c)
+        xv[s][c] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xr, voff[c], so, 0));
+      yv[s] = __builtin_bit_cast(
+          double, __builtin_amdgcn_raw_buffer_load_b64(yr, q * 8, __builtin_amdgcn_readfirstlane((r0 + 4 * s) * 8), 0));
     }
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-#pragma unroll
-      for (int c = 0; c < NT; ++c) asm volatile("" : "+v"(xv[s][c]));
-      asm volatile("" : "+v"(yv[s]));
-    }
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const bool valid = r0 + 4 * s + q < nrows;
+      // (a row past the chunk loads 0, which standardisation would shift)
+      const bool valid = (FULL && !STD) || r0 + 4 * s + q < nrows;
       double v[NT];
 #pragma unroll
       for (int c = 0; c < NT; ++c) {
         double x = xv[s][c];
         if constexpr (STD) x = (x - cen[c]) * isc[c];
-        if constexpr (FULL) {
-          v[c] = valid ? x : 0.0;
+        if constexpr (FULL && !STD) {
+          v[c] = x;
         } else {
           const bool one = c == 0 && icpt;
           v[c] = valid && (fin[c] || one) ? (one ? 1.0 : x) : 0.0;
         }
       }
-      const double y = valid ? yv[s] : 0.0;
+      const double y = yv[s];  // 0 past the chunk
 #pragma unroll
       for (int c = 0; c < NT; ++c) gacc[c] = fma(v[c], y, gacc[c]);
-      if (fl == 0) ll = fma(-0.5 * y, y, ll);  // each row once (lane fl = 0 of its group)
+      ll = fma(-0.5 * y, y, ll);  // each row in its 16 lanes: the sum is scaled by 1/16
 #pragma unroll
       for (int I = 0; I < NT; ++I)
 #pragma unroll
@@ -142,8 +155,8 @@ __global__ __launch_bounds__(64 * kOlsWaves) void ols_stream_kernel(const PassAr
     if (q == 0) a.slab_g[(int64_t)chunk * PMAX + 16 * c + fl] = g;
   }
 #pragma unroll
-  for (int o = 16; o < 64; o <<= 1) ll += __shfl_xor(ll, o);
-  if (lane == 0) a.slab_ll[chunk] = ll;
+  for (int o = 1; o < 64; o <<= 1) ll += __shfl_xor(ll, o);
+  if (lane == 0) a.slab_ll[chunk] = ll * 0.0625;  // 16 lanes per row (exact: a power of 2)
 }
 
 template <int NT>
