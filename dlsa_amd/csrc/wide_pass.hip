@@ -24,14 +24,35 @@
 //   wide_newton_kernel  one 1024-thread workgroup per partition: step
 //                       control, publish Sig_inv, blocked right-looking
 //                       Cholesky (32-column panels staged in LDS, trailing
-//                       update on fp64 MFMA), blocked triangular solves,
-//                       update / convergence (same state machine as
-//                       newton_solve.hip).
+//                       update on fp64 MFMA, the next diagonal block
+//                       factored under the current trailing update),
+//                       blocked triangular solves, update / convergence
+//                       (same state machine as newton_solve.hip).
 #include <math.h>
 #include <stdlib.h>
 
 #include "dlsa_internal.hpp"
 #include "irls_wave_impl.hpp"  // wv_* wave helpers
+
+// wide Newton: lookahead Cholesky with inverted diagonal blocks (1) or the
+// round-4 panel sequence (0, A/B)
+#ifndef DLSA_WN_LOOKAHEAD
+#define DLSA_WN_LOOKAHEAD 1
+#endif
+
+// Profiling build (DLSA_WN_PROF, tools/build_variants.sh wnprof): cycle stamps
+// of the wide Newton kernel's stages, summed over workgroup runs into
+// g_wn_prof (one vector atomic per stage per run; wave 1 stamps its share of
+// the trailing update)
+#ifdef DLSA_WN_PROF
+static __device__ unsigned long long g_wn_prof[16];
+#define WN_STAMP(v) uint64_t v = __builtin_readcyclecounter()
+#define WN_ADD(i, d) \
+  if (lane == 0) atomicAdd(&g_wn_prof[i], (unsigned long long)(d))
+#else
+#define WN_STAMP(v)
+#define WN_ADD(i, d)
+#endif
 
 namespace dlsa {
 
@@ -902,6 +923,7 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
   if (a.phase[k] != PHASE_F32 && a.phase[k] != PHASE_F64) return;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int P = a.P, PP = GT * wa.NB;
+  WN_STAMP(t_k0);
   double* L11 = sm;             // [CB][LDP] diagonal block
   double* Lp = L11 + CB * LDP;  // [PP][LDP] panel below it (scratch in the solves)
   double* g = Lp + PP * LDP;    // [PP]
@@ -987,6 +1009,299 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
   if (a.eval_only) return;
   __syncthreads();
 
+#if DLSA_WN_LOOKAHEAD
+  WN_STAMP(t_f0);
+  if (wid == 0) { WN_ADD(9, t_f0 - t_k0); WN_ADD(8, 1); }
+  // 4. blocked Cholesky H = L L^T (lower, in place), one panel of lookahead:
+  // while waves 1..15 apply panel jb's trailing update to the columns past
+  // the next panel, wave 0 factors the next diagonal block (its columns were
+  // updated first), so the pivot chain of a block runs under the previous
+  // panel's MFMA work instead of between panels.  The reciprocal pivots are
+  // kept, so the panel solve and the triangular solves multiply instead of
+  // divide on their dependency chains.
+  const int fl = lane & 15, kq = lane >> 4;
+  const int wv = __builtin_amdgcn_readfirstlane(wid);
+  // wave 0: factor diagonal block jb (lane i = row i; column j of L goes
+  // through L11, column-major, to the other lanes; 1 / L[j][j] in its padding
+  // slot); lanes 32..63 repeat lanes 0..31 and store the same values
+  auto factor_diag = [&](int jb) {
+    // the lane index re-defined opaquely: otherwise the compiler hoists the
+    // lane-compare masks of the unrolled pivots and spills them (as in
+    // newton_solve.hip)
+    int lv = lane;
+    asm volatile("" : "+v"(lv));
+    const int i = lv & 31;
+    const double* hr = H + (int64_t)(jb + i) * PP + jb;
+    double row[CB];
+#pragma unroll
+    for (int c = 0; c < CB; ++c) {
+      const double hv = hr[c];
+      row[c] = c <= i ? hv : 0.0;
+    }
+    double dg = 1.0;  // this lane's diagonal entry L[i][i]
+#pragma unroll
+    for (int j = 0; j < CB; ++j) {
+      const double d = bcast_f64(row[j], j);
+      // 1 / sqrt(d) by v_rsq_f64 + two Newton steps (~1 ulp), L_jj = d / sqrt(d)
+      // (NaN for a pivot that is not > 0 and finite: the flag below)
+      double il = __builtin_amdgcn_rsq(d);
+#pragma unroll
+      for (int nr = 0; nr < 2; ++nr) il = fma(il, fma(-0.5 * d * il, il, 0.5), il);
+      const double ljj = d * il;
+      dg = i == j ? ljj : dg;
+      row[j] = i > j ? row[j] * il : (i == j ? ljj : row[j]);
+      L11[j * LDP + CB] = il;  // 1 / L[j][j] in the padding slot
+#pragma unroll
+      for (int c = j + 1; c < CB; ++c) {
+        const double lcj = bcast_f64(row[j], c);  // L[c][j], row c's lane
+        if (c <= i) row[c] = fma(-row[j], lcj, row[c]);
+      }
+    }
+    double* hw = H + (int64_t)(jb + i) * PP + jb;
+#pragma unroll
+    for (int c = 0; c < CB; ++c) {
+      hw[c] = row[c];
+      L11[c * LDP + i] = row[c];  // column-major for the panel solve
+    }
+    if (__ballot(!(dg > 0.0 && isfinite(dg))) != 0 && lv == 0) *flag = 1;
+  };
+  // L21 = A21 L11^-T by right-looking substitution, one thread per row of the
+  // panel (staged in Lp by coalesced loads): the chain per column is one
+  // multiply by the stored reciprocal pivot, the updates of the later columns
+  // are independent FMAs
+  auto panel_copy = [&](int jb, int rest, bool to_lds) {
+    for (int e = tid; e < rest * CB; e += 1024) {
+      const int r = e >> 5, c = e & 31;
+      double* hp = H + (int64_t)(jb + CB + r) * PP + jb + c;
+      if (to_lds)
+        Lp[r * LDP + c] = *hp;
+      else
+        *hp = Lp[r * LDP + c];
+    }
+  };
+  // substitution of columns c0 .. c0 + 15 of every panel row (thread per row)
+  auto subst16 = [&](int rest, int c0) {
+    if (tid < rest) {
+      double* lr = Lp + tid * LDP + c0;
+      double v[16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) v[c] = lr[c];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        v[c] *= L11[(c0 + c) * LDP + CB];
+#pragma unroll
+        for (int c2 = c + 1; c2 < 16; ++c2) v[c2] = fma(-v[c], L11[(c0 + c) * LDP + c0 + c2], v[c2]);
+      }
+#pragma unroll
+      for (int c = 0; c < 16; ++c) lr[c] = v[c];
+    }
+  };
+  // the panel solve in two column halves: X1 by substitution, the second
+  // half's right-hand side less X1 L[16..32)[0..16)^T on the fp64 MFMA, X2 by
+  // substitution (16 values per thread: the broadcast reads pipeline)
+  auto trsm = [&](int rest) {
+    subst16(rest, 0);
+    __syncthreads();
+    for (int ti = wv; ti < rest / 16; ti += 16) {
+      d4w acc = d4w{0, 0, 0, 0};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Lp[(16 * ti + fl) * LDP + 4 * s4 + kq],
+                                                   L11[(4 * s4 + kq) * LDP + 16 + fl], acc, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Lp[(16 * ti + kq + 4 * r) * LDP + 16 + fl] -= acc[r];
+    }
+    __syncthreads();
+    subst16(rest, 16);
+  };
+  // A22 -= L21 L21^T on lower 16x16 tiles: the two tile columns of the next
+  // panel (cols01) or the rest; UT tiles per wave at a time (their C reads
+  // issued together: one L2 / MALL latency for UT read-modify-writes); tiles
+  // past the end recompute the last tile and skip the store
+  auto trail = [&](int jb, int m, bool cols01, int w0, int nw) {
+    const int ntiles = cols01 ? 2 * m - 1 : (m - 2) * (m - 1) / 2;
+    constexpr int UT = 4;
+    for (int t0 = w0; t0 < ntiles; t0 += nw * UT) {
+      int ti[UT], tj[UT];
+      d4w c[UT];
+#pragma unroll
+      for (int u = 0; u < UT; ++u) {
+        const int t = min(t0 + nw * u, ntiles - 1);
+        if (cols01) {
+          ti[u] = t < m ? t : t - m + 1;
+          tj[u] = t < m ? 0 : 1;
+        } else {
+          tile_ij(t, ti[u], tj[u]);
+          ti[u] += 2;
+          tj[u] += 2;
+        }
+        const double* cp = H + (int64_t)(jb + CB + 16 * ti[u] + kq) * PP + jb + CB + 16 * tj[u] + fl;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) c[u][r] = cp[4 * r * PP];
+      }
+#pragma unroll
+      for (int u = 0; u < UT; ++u) {
+        d4w acc = d4w{0, 0, 0, 0};
+#pragma unroll
+        for (int s = 0; s < CB / 4; ++s) {
+          const double av = Lp[(16 * ti[u] + fl) * LDP + 4 * s + kq];
+          const double bv = Lp[(16 * tj[u] + fl) * LDP + 4 * s + kq];
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+        }
+        if (t0 + nw * u < ntiles) {
+          double* cp = H + (int64_t)(jb + CB + 16 * ti[u] + kq) * PP + jb + CB + 16 * tj[u] + fl;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) cp[4 * r * PP] = c[u][r] - acc[r];
+        }
+      }
+    }
+  };
+  if (wv == 0) factor_diag(0);
+  __syncthreads();
+  {
+    WN_STAMP(t1);
+    if (wid == 0) WN_ADD(0, t1 - t_f0);
+  }
+  if (!*flag) {
+    for (int jb = 0; jb + CB < PP; jb += CB) {
+      const int m = (PP - jb - CB) / 16;
+      WN_STAMP(ta);
+      panel_copy(jb, PP - jb - CB, true);
+      __syncthreads();
+      trsm(PP - jb - CB);
+      __syncthreads();
+      WN_STAMP(tb);
+      trail(jb, m, true, wv, 16);
+      panel_copy(jb, PP - jb - CB, false);  // L21 to H for the solves
+      __syncthreads();
+      WN_STAMP(tc);
+      if (wv == 0)
+        factor_diag(jb + CB);
+      else
+        trail(jb, m, false, wv - 1, 15);
+      WN_STAMP(td);
+      __syncthreads();
+      WN_STAMP(te);
+      if (wid == 0) {
+        WN_ADD(1, tb - ta);
+        WN_ADD(2, tc - tb);
+        WN_ADD(3, td - tc);
+        WN_ADD(4, te - td);
+      }
+      if (wid == 1) WN_ADD(5, td - tc);
+      if (*flag) break;  // uniform
+    }
+  }
+  if (*flag) {
+    if (a.subsample) {
+      level_fail();
+      return;
+    }
+    if (tid == 0) {
+      if (phase != PHASE_F64 && a.family == FAMILY_LOGISTIC) {
+        // approximate Hessian lost definiteness: redo this point in fp64
+        a.phase[k] = PHASE_F64;
+        a.iters[k] = it + 1;
+        a.stall[k] = 0;
+        a.dm_prev[k] = 0.0;
+        atomicAdd(&a.counters[PHASE_F64], 1);
+      } else {
+        a.status[k] = DLSA_STATUS_SINGULAR;
+      }
+    }
+    return;
+  }
+
+  // 5a. forward solve L z = g, 32-row blocks: the diagonal block by one wave
+  // (lane i = row i, reciprocal pivots off the chain), then the rows below take
+  // the block's terms (their L entries loaded before the block is final)
+  WN_STAMP(t_s0);
+  for (int f = tid; f < PP; f += 1024) z[f] = g[f];
+  __syncthreads();
+  for (int jb = 0; jb < PP; jb += CB) {
+    const int rest = PP - jb - CB;
+    const int rr = tid - 64;  // waves 1..: the rows below, loaded before the block is final
+    const int ib = jb + CB + rr;
+    double hv[CB];
+    if (wv >= 1 && (wv - 1) * 64 < rest) {
+      const double* hb = H + (int64_t)min(ib, PP - 1) * PP + jb;
+#pragma unroll
+      for (int c = 0; c < CB; ++c) hv[c] = hb[c];
+    }
+    if (wv == 0) {
+      const int i = lane & 31;
+      const double* hr = H + (int64_t)(jb + i) * PP + jb;
+      double lrow[CB];
+#pragma unroll
+      for (int c = 0; c < CB; ++c) lrow[c] = hr[c];  // upper part: zeros (factor_diag)
+      const double ri = 1.0 / hr[i];
+      double zi = z[jb + i];
+#pragma unroll
+      for (int c = 0; c < CB; ++c) {
+        if (i == c) zi *= ri;
+        const double zc = bcast_f64(zi, c);
+        if (i > c) zi = fma(-lrow[c], zc, zi);
+      }
+      z[jb + i] = zi;
+    }
+    __syncthreads();
+    if (wv >= 1 && rr < rest) {
+      double s = z[ib];
+#pragma unroll
+      for (int c = 0; c < CB; ++c) s = fma(-hv[c], z[jb + c], s);
+      z[ib] = s;
+    }
+    __syncthreads();
+  }
+  WN_STAMP(t_s1);
+  // 5b. backward solve L^T d = z (d overwrites z): u_c = sum_{i >= jb + CB}
+  // L[i][jb + c] d_i in fixed order (4 rows in flight per thread), then
+  // L11^T d_b = z_b - u by one wave (lane c = unknown c)
+  for (int jb = PP - CB; jb >= 0; jb -= CB) {
+    {
+      const int c = tid & 31, grp = tid >> 5;
+      double s = 0.0;
+      int i = jb + CB + grp;
+      for (; i + 96 < PP; i += 128) {
+        const double h0 = H[(int64_t)i * PP + jb + c], h1 = H[(int64_t)(i + 32) * PP + jb + c];
+        const double h2 = H[(int64_t)(i + 64) * PP + jb + c], h3 = H[(int64_t)(i + 96) * PP + jb + c];
+        s = fma(h0, z[i], s);
+        s = fma(h1, z[i + 32], s);
+        s = fma(h2, z[i + 64], s);
+        s = fma(h3, z[i + 96], s);
+      }
+      for (; i < PP; i += 32) s = fma(H[(int64_t)i * PP + jb + c], z[i], s);
+      L11[grp * LDP + c] = s;
+    }
+    __syncthreads();
+    if (wv == 0) {
+      const int c = lane & 31;
+      double lcol[CB];  // column c of L11: L[r][c] (zero above the diagonal)
+#pragma unroll
+      for (int r = 0; r < CB; ++r) lcol[r] = H[(int64_t)(jb + r) * PP + jb + c];
+      const double rc = 1.0 / H[(int64_t)(jb + c) * PP + jb + c];
+      double u = 0.0;
+#pragma unroll
+      for (int q = 0; q < 32; ++q) u += L11[q * LDP + c];
+      double v = z[jb + c] - u;
+#pragma unroll
+      for (int r = CB - 1; r >= 0; --r) {
+        if (c == r) v *= rc;
+        const double dr = bcast_f64(v, r);
+        if (c < r) v = fma(-lcol[r], dr, v);
+      }
+      z[jb + c] = v;
+    }
+    __syncthreads();
+  }
+  {
+    WN_STAMP(t_s2);
+    if (wid == 0) {
+      WN_ADD(6, t_s1 - t_s0);
+      WN_ADD(7, t_s2 - t_s1);
+    }
+  }
+#else
   // 4. blocked Cholesky H = L L^T, lower, in place -------------------------
   const int fl = lane & 15, kq = lane >> 4;
   for (int jb = 0; jb < PP; jb += CB) {
@@ -1165,6 +1480,7 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
     }
     __syncthreads();
   }
+#endif  // DLSA_WN_LOOKAHEAD
 
   // 6. update + convergence (newton_solve.hip step 6) ------------------------
   double dm = 0.0, tm = 0.0, tg = 0.0;
@@ -1246,6 +1562,15 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
   a.phase[k] = ph;
   atomicAdd(&a.counters[ph], 1);
 }
+
+#ifdef DLSA_WN_PROF
+extern "C" int dlsa_wn_prof_read(unsigned long long* out) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wn_prof), 16 * 8) != hipSuccess) return -1;
+  unsigned long long z[16] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_wn_prof), z, 16 * 8) == hipSuccess ? 0 : -1;
+}
+#endif
 
 // ---------------------------------------------------------------------------
 // launchers

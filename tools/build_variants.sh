@@ -43,6 +43,8 @@ for v in "$@"; do
     oz6) D=DLSA_OZ_LEVELS=6 ;;
     cmabl) D=DLSA_CM_ABLATE=1 ;;
     olswave) D=DLSA_OLS_STREAM=0 ;;
+    wnold) D=DLSA_WN_LOOKAHEAD=0 ;;
+    wnprof) D=DLSA_WN_PROF=1 ;;
     nt) D=DLSA_X_DMA_AUX=2 ;;
     dma0) D=DLSA_X_DMA_AUX=0 ;;
     sc1) D=DLSA_X_DMA_AUX=1 ;;
@@ -53,6 +55,7 @@ for v in "$@"; do
     oz*|ozs*) ONLY='["irls_oz.hip", "irls_oz_g2.hip"]' ;;
     solve*) ONLY='["newton_solve.hip"]' ;;
     olswave) ONLY='["ols_stream.hip"]' ;;
+    wn*) ONLY='["wide_pass.hip"]' ;;
     cmabl) ONLY='["irls_coop_g1.hip", "irls_coop_g2.hip", "irls_coop_g3.hip", "irls_coop_g4.hip", "irls_coop_g5.hip", "irls_coop_g6.hip"]' ;;
     ols*|wslot3) ONLY='["irls_wave.hip", "irls_wave_g2.hip"]' ;;
   esac
