@@ -56,6 +56,7 @@ for v in "$@"; do
     solve*) ONLY='["newton_solve.hip"]' ;;
     olswave) ONLY='["ols_stream.hip"]' ;;
     wn*) ONLY='["wide_pass.hip"]' ;;
+    knobs) ONLY='["capi.hip"]' ;;
     cmabl) ONLY='["irls_coop_g1.hip", "irls_coop_g2.hip", "irls_coop_g3.hip", "irls_coop_g4.hip", "irls_coop_g5.hip", "irls_coop_g6.hip"]' ;;
     ols*|wslot3) ONLY='["irls_wave.hip", "irls_wave_g2.hip"]' ;;
   esac
