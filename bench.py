@@ -356,6 +356,11 @@ def main():
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        # release the previous step's outputs before the next fit allocates
+        # its own, so the caching allocator reuses their blocks: a fresh
+        # device allocation held the next launches back by ~5 ms
+        # (profiles/r05y_c5_host_gaps.txt)
+        fit = None
         fit, est, support, K_red, n_red = step(True)
         stats_acc.append(fit.stats)
     torch.cuda.synchronize()
