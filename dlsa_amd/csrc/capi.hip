@@ -145,6 +145,13 @@ static int32_t* pinned_staging(size_t n_i32) {
   return buf;
 }
 
+// fewest rows of a warm-start level per parameter (DLSA_LEVEL_ROWS_PER_P
+// overrides in knob builds, schedule sweeps)
+static int64_t level_rows_per_param() {
+  if (const char* e = env_knob("DLSA_LEVEL_ROWS_PER_P")) return std::max<int64_t>(1, atoll(e));
+  return 64;
+}
+
 static double warm_level_tol(bool fused) {
   if (const char* e = env_knob("DLSA_LEVEL_TOL")) return atof(e);
   return fused ? 0.2 : 0.1;
@@ -351,7 +358,7 @@ static std::vector<WidePlans> wide_level_plans(const int64_t* offsets, int K, in
   std::vector<WidePlans> plans;
   const int P = p + (intercept ? 1 : 0);
   if (levels) {
-    const int64_t min_rows = std::max<int64_t>(2048, 64LL * P);
+    const int64_t min_rows = std::max<int64_t>(2048, level_rows_per_param() * P);
     for (double frac : warm_level_fracs(false)) {
       WidePlans q;
       make_wide_plans(offsets, K, p, intercept, rows_per_chunk, q, frac, min_rows);
@@ -919,7 +926,7 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
   // warm-start levels: Newton on row prefixes (1/16, 1/4) before all rows
   std::vector<Plan> plans;
   if (family == FAMILY_LOGISTIC && opt.warm_start) {
-    const int64_t min_rows = std::max<int64_t>(2048, 64LL * pl.P);
+    const int64_t min_rows = std::max<int64_t>(2048, level_rows_per_param() * pl.P);
     for (double frac : warm_level_fracs(true)) {
       Plan q;
       make_plan(offsets, K, p, fit_intercept, opt.rows_per_chunk, q, frac, min_rows);
@@ -1300,7 +1307,7 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
   opt.warm_start = opt.warm_start && K > 0 && n_total / K >= (int64_t(1) << 19);
   if (const char* e = env_knob("DLSA_WARM_START")) opt.warm_start = atoi(e);
   if (opt.warm_start) {
-    const int64_t min_rows = std::max<int64_t>(2048, 64LL * P);
+    const int64_t min_rows = std::max<int64_t>(2048, level_rows_per_param() * P);
     for (double frac : warm_level_fracs(true)) {
       Plan qn;
       const int64_t lr = level_rows(offsets, K, frac, min_rows);
