@@ -306,6 +306,35 @@ def test_ols_small_p_geometry_vs_oracle(torch_cuda, M, p, fi, std):
         assert _rel(fit.sig_inv[k].cpu(), o["Sig_inv"]) < 1e-12
 
 
+@pytest.mark.parametrize("p,fi,std", [(16, False, False), (48, False, True), (47, True, False),
+                                      (33, True, True)])
+def test_ols_stream_short_chunks_vs_oracle(torch_cuda, M, p, fi, std):
+    """OLS stream kernel (ols_stream.hip) with chunks of 7 rows: every chunk
+    ends inside a k-step group, so its rows past the chunk come from the
+    bounds-checked buffer loads (read as 0, selected away under
+    standardisation); P = 16 and 48 without intercept take the FULL path.
+    An empty partition gives the zero frame and status 3."""
+    rs = np.random.RandomState(200 + p)
+    sizes = [517, 0, 96, 1031]
+    n = sum(sizes)
+    X = rs.rand(n, p) * 3.0 - 0.5
+    y = X @ rs.randn(p) + 0.4 + 0.1 * rs.randn(n)
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    center = X.mean(0) if std else None
+    scale = X.std(0) if std else None
+    fit = M.ols_model_batched(X, y, off, fit_intercept=fi, center=center, scale=scale,
+                              rows_per_chunk=7)
+    st = fit.status.cpu().numpy()
+    assert st[1] == 3
+    assert np.all(fit.sig_inv[1].cpu().numpy() == 0)
+    Xs = (X - center) / scale if std else X
+    for k in (0, 2, 3):
+        assert st[k] == 0
+        o = O.ols_fit(Xs[off[k]:off[k + 1]], y[off[k]:off[k + 1]], fit_intercept=fi)
+        assert _rel(fit.theta[k].cpu(), o["coef"]) < REL
+        assert _rel(fit.sig_inv[k].cpu(), o["Sig_inv"]) < 1e-12
+
+
 @pytest.mark.parametrize("p,fi,std", [(10, False, False), (100, True, False), (37, True, True)])
 def test_loglik_eval_vs_oracle(torch_cuda, M, p, fi, std):
     """Evaluation pass (models.py:151-225): per-partition log-likelihood of 4
