@@ -159,9 +159,17 @@ __global__ __launch_bounds__(64 * kOlsWaves) void ols_stream_kernel(const PassAr
   if (lane == 0) a.slab_ll[chunk] = ll * 0.0625;  // 16 lanes per row (exact: a power of 2)
 }
 
+// k-steps (4 rows each) whose loads are issued together.  At NT = 4 (config
+// 4), 8 (2 waves per SIMD, 32 rows of loads in flight per wave) measured
+// 11.96-12.26 ms per pass against 12.18-12.34 for 4 (3 waves per SIMD),
+// 12.25-12.31 for 12 and 12.3-12.6 for 2 (4 waves per SIMD); 16 measured
+// 13.5 ms (profiles/r05ok_ols_ks_sweep.jsonl).  DLSA_OLS_KS: A/B builds.
+#ifndef DLSA_OLS_KS
+#define DLSA_OLS_KS 8
+#endif
 template <int NT>
 hipError_t launch_ols_nt(const PassArgs& a, bool standardize, int n_chunks, hipStream_t s) {
-  constexpr int KS = NT <= 2 ? 8 : 4;
+  constexpr int KS = DLSA_OLS_KS;
   const dim3 grid((n_chunks + kOlsWaves - 1) / kOlsWaves), block(64 * kOlsWaves);
   const bool full = a.intercept == 0 && a.p == 16 * NT;
   if (standardize) {

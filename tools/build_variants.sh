@@ -44,6 +44,11 @@ for v in "$@"; do
     cmabl) D=DLSA_CM_ABLATE=1 ;;
     olswave) D=DLSA_OLS_STREAM=0 ;;
     wnold) D=DLSA_WN_LOOKAHEAD=0 ;;
+    olsks2) D=DLSA_OLS_KS=2 ;;
+    olsks2k) D="DLSA_OLS_KS=2 -DDLSA_ENV_KNOBS=1" ;;
+    olsks8) D=DLSA_OLS_KS=8 ;;
+    olsks12) D=DLSA_OLS_KS=12 ;;
+    olsks16) D=DLSA_OLS_KS=16 ;;
     wnprof) D=DLSA_WN_PROF=1 ;;
     nt) D=DLSA_X_DMA_AUX=2 ;;
     dma0) D=DLSA_X_DMA_AUX=0 ;;
@@ -54,7 +59,8 @@ for v in "$@"; do
   case $v in
     oz*|ozs*) ONLY='["irls_oz.hip", "irls_oz_g2.hip"]' ;;
     solve*) ONLY='["newton_solve.hip"]' ;;
-    olswave) ONLY='["ols_stream.hip"]' ;;
+    olswave|olsks2|olsks8|olsks12|olsks16) ONLY='["ols_stream.hip"]' ;;
+    olsks2k) ONLY='["ols_stream.hip", "capi.hip"]' ;;
     wn*) ONLY='["wide_pass.hip"]' ;;
     knobs) ONLY='["capi.hip"]' ;;
     cmabl) ONLY='["irls_coop_g1.hip", "irls_coop_g2.hip", "irls_coop_g3.hip", "irls_coop_g4.hip", "irls_coop_g5.hip", "irls_coop_g6.hip"]' ;;
