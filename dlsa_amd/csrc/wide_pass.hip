@@ -39,6 +39,10 @@
 #ifndef DLSA_WN_LOOKAHEAD
 #define DLSA_WN_LOOKAHEAD 1
 #endif
+// rows per wave and step of the wide row pass (A/B builds)
+#ifndef DLSA_WIDE_ROW_U
+#define DLSA_WIDE_ROW_U 4
+#endif
 
 // Profiling build (DLSA_WN_PROF, tools/build_variants.sh wnprof): cycle stamps
 // of the wide Newton kernel's stages, summed over workgroup runs into
@@ -136,7 +140,7 @@ __global__ __launch_bounds__(256) void wide_row_kernel(const WideArgs a) {
   uint32_t zmx[MB];
 #pragma unroll
   for (int m = 0; m < MB; ++m) zmx[m] = 0u;
-  constexpr int U = 4;  // rows per wave per step (all U rows' loads in flight)
+  constexpr int U = DLSA_WIDE_ROW_U;  // rows per wave per step (all U rows' loads in flight)
   for (int base = wid * U; base < nrows; base += 4 * U) {
     double xv[U][MB], yv[U];
 #pragma unroll

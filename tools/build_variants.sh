@@ -50,6 +50,8 @@ for v in "$@"; do
     olsks12) D=DLSA_OLS_KS=12 ;;
     olsks16) D=DLSA_OLS_KS=16 ;;
     wnprof) D=DLSA_WN_PROF=1 ;;
+    wrow2) D=DLSA_WIDE_ROW_U=2 ;;
+    wrow8) D=DLSA_WIDE_ROW_U=8 ;;
     nt) D=DLSA_X_DMA_AUX=2 ;;
     dma0) D=DLSA_X_DMA_AUX=0 ;;
     sc1) D=DLSA_X_DMA_AUX=1 ;;
@@ -61,7 +63,7 @@ for v in "$@"; do
     solve*) ONLY='["newton_solve.hip"]' ;;
     olswave|olsks2|olsks8|olsks12|olsks16) ONLY='["ols_stream.hip"]' ;;
     olsks2k) ONLY='["ols_stream.hip", "capi.hip"]' ;;
-    wn*) ONLY='["wide_pass.hip"]' ;;
+    wn*|wrow*) ONLY='["wide_pass.hip"]' ;;
     knobs) ONLY='["capi.hip"]' ;;
     cmabl) ONLY='["irls_coop_g1.hip", "irls_coop_g2.hip", "irls_coop_g3.hip", "irls_coop_g4.hip", "irls_coop_g5.hip", "irls_coop_g6.hip"]' ;;
     ols*|wslot3) ONLY='["irls_wave.hip", "irls_wave_g2.hip"]' ;;
