@@ -222,9 +222,10 @@ int dlsa_logistic_fit_batched_ex(const double* X, const double* y,
  *   theta_k = (X_k^T X_k)^-1 X_k^T y_k,  Sig_inv_k = X_k^T X_k,
  *   sig_inv_theta_k = Sig_inv_k theta_k (= X_k^T y_k),
  *   rss_k = sum (y - X theta_k)^2.
- * One fused fp64 pass over X (same kernel as the logistic pass with w = 1)
- * plus one per-partition Cholesky solve.  opt may be NULL; its hessian_mode
- * is ignored (always fp64).
+ * One fp64 pass over X at theta = 0 (w = 1; P <= 64: X streamed straight
+ * into the fp64-MFMA operands, ols_stream.hip; larger P: the logistic pass's
+ * kernels with w = 1) plus one per-partition Cholesky solve.  opt may be
+ * NULL; its hessian_mode is ignored (always fp64).
  */
 int dlsa_ols_fit_batched(const double* X, const double* y, const int64_t* offsets,
                          int32_t K, int32_t p, int32_t fit_intercept,
