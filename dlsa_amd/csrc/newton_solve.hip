@@ -18,6 +18,11 @@
 
 #include "dlsa_internal.hpp"
 
+// Newton steps refining v_rsq_f64 in the diagonal-block factor (A/B builds)
+#ifndef DLSA_SOLVE_RSQ_STEPS
+#define DLSA_SOLVE_RSQ_STEPS 2
+#endif
+
 // Profiling-only phase timestamps of partition 0 (tools/build_variants.sh
 // solveprof; product build 0): printf of shader-clock deltas per phase.
 #ifndef DLSA_SOLVE_PROFILE
@@ -265,7 +270,7 @@ __global__ __launch_bounds__(NTHR) void newton_solve_kernel(const SolveArgs a) {
           // ~2x the dependent latency)
           double il = __builtin_amdgcn_rsq(dkk);
 #pragma unroll
-          for (int nr = 0; nr < 2; ++nr) il = fma(il, fma(-0.5 * dkk * il, il, 0.5), il);
+          for (int nr = 0; nr < DLSA_SOLVE_RSQ_STEPS; ++nr) il = fma(il, fma(-0.5 * dkk * il, il, 0.5), il);
           const double lkk = dkk * il;
           if (lv == kk) ild = il;
           av[kk] = (i > kk) ? av[kk] * il : (i == kk ? lkk : av[kk]);

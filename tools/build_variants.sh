@@ -18,6 +18,8 @@ for v in "$@"; do
     cat16) D=DLSA_CAT_ABLATE=16 ;;
     solveprof) D=DLSA_SOLVE_PROFILE=1 ;;
     solveblk) D=DLSA_SOLVE_BLOCKED=1 ;;
+    solversq1) D=DLSA_SOLVE_RSQ_STEPS=1 ;;
+    solversq0) D=DLSA_SOLVE_RSQ_STEPS=0 ;;
     cat31) D=DLSA_CAT_ABLATE=31 ;;
     fab1) D=DLSA_FUSED_ABLATE=1 ;;
     wslot3) D=DLSA_WAVE_NSLOT=3 ;;
