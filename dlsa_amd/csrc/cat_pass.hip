@@ -89,27 +89,30 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
   double* stdv = th + kCatPMax;            // 2 x kCatQMax: center, 1 / scale
   double* red = stdv + 2 * kCatQMax;       // NW x NR, then NR final sums
 
-  // factor / pair tables in LDS: re-read (broadcast) every row instead of
-  // pinning ~100 loop-invariant values in registers
-  __shared__ int32_t tb[5 * kCatMaxFactors + 2 * kCatMaxPairs];
-  int32_t* t_nlev = tb;
-  int32_t* t_doff = tb + kCatMaxFactors;
-  int32_t* t_ndoff = tb + 2 * kCatMaxFactors;
-  int32_t* t_ndrep = tb + 3 * kCatMaxFactors;
-  int32_t* t_goff = tb + 4 * kCatMaxFactors;
-  int32_t* t_proff = tb + 5 * kCatMaxFactors;
-  int32_t* t_prrep = t_proff + kCatMaxPairs;
-  for (int i = tid; i < kCatMaxFactors; i += NTHR) {
-    t_nlev[i] = a.nlev[i];
-    t_doff[i] = a.doff[i];
-    t_ndoff[i] = a.nd_off[i];
-    t_ndrep[i] = a.nd_rep[i] - 1;  // replica mask
-    t_goff[i] = a.g_off[i];
+  // factor / pair tables in LDS, re-read (broadcast) every row instead of
+  // pinning ~100 loop-invariant values in registers: one 16-byte record per
+  // factor {replica mask, levels, nd offset, gradient offset} and per pair in
+  // the row loop's (f, g) order for FM {offset, replica mask, L_f, L_g}, at
+  // compile-time positions; records past F are zero
+  constexpr int NPM = FM * (FM - 1) / 2;
+  __shared__ int4 ftab[kCatMaxFactors + 1];
+  __shared__ int4 ptab[kCatMaxPairs + 1];
+  __shared__ int32_t t_doff[kCatMaxFactors];
+  for (int i = tid; i <= FM; i += NTHR)
+    ftab[i] = i < F ? make_int4(a.nd_rep[i] - 1, a.nlev[i], a.nd_off[i], a.g_off[i])
+                    : make_int4(0, 0, 0, 0);
+  for (int i = tid; i <= NPM; i += NTHR) {
+    int f = 0, g = i;  // position i = cat_pair(f, g, FM)
+    while (f < FM - 1 && g >= FM - 1 - f) g -= FM - 1 - f, ++f;
+    g += f + 1;
+    int4 v = make_int4(0, 0, 0, 0);
+    if (i < NPM && g < F) {
+      const int pi = cat_pair(f, g, F);
+      v = make_int4(a.pr_off[pi], a.pr_rep[pi] - 1, a.nlev[f], a.nlev[g]);
+    }
+    ptab[i] = v;
   }
-  for (int i = tid; i < kCatMaxPairs; i += NTHR) {
-    t_proff[i] = a.pr_off[i];
-    t_prrep[i] = a.pr_rep[i] - 1;
-  }
+  for (int i = tid; i < kCatMaxFactors; i += NTHR) t_doff[i] = a.doff[i];
   for (int i = tid; i < a.hist_doubles; i += NTHR) hist[i] = 0ull;
   for (int i = tid; i < kCatPMax; i += NTHR) th[i] = i < P ? a.theta[(int64_t)part * P + i] : 0.0;
   if (STD && tid < kCatQMax) {
@@ -189,11 +192,18 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
     }
 
     // one-hot blocks: fixed-point histograms in LDS
+    // The record of factor f + 1 (pair p + 1) is read before factor f's (pair
+    // p's) adds are issued: LDS operations complete in order, so a record read
+    // after the adds would wait for every one of them (an s_waitcnt
+    // lgkmcnt(0), a drain of the LDS queue, per factor and pair); read ahead,
+    // the wait covers the read alone.
+    int4 tf = ftab[0];
 #pragma unroll
     for (int f = 0; f < FM; ++f) {
+      const int4 tn = ftab[f + 1];
       if (f < F && cv[f] > 0) {
-        const int slot = (lane & t_ndrep[f]) * t_nlev[f] + cv[f] - 1;
-        unsigned long long* h = hist + t_ndoff[f] + slot * a.nd_stride;
+        const int slot = (lane & tf.x) * tf.y + cv[f] - 1;
+        unsigned long long* h = hist + tf.z + slot * a.nd_stride;
         if constexpr (!(DLSA_CAT_ABLATE & 1)) {
           lds_add(h, w, hsc[0]);
 #pragma unroll
@@ -204,19 +214,19 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
             if (i >= ic && i < Qn) lds_add(h + 1 + (i - ic), w * xv[i], sc);
           }
         }
-        if constexpr (!(DLSA_CAT_ABLATE & 4)) lds_add(hist + t_goff[f] + slot, res, hsc[1]);
+        if constexpr (!(DLSA_CAT_ABLATE & 4)) lds_add(hist + tf.w + slot, res, hsc[1]);
       }
+      tf = tn;
     }
+    int4 tp = ptab[0];
 #pragma unroll
     for (int f = 0; f < FM; ++f)
 #pragma unroll
       for (int g = f + 1; g < FM; ++g) {
-        if (!(DLSA_CAT_ABLATE & 2) && g < F && cv[f] > 0 && cv[g] > 0) {
-          const int pi = cat_pair(f, g, F);
-          const int rep = lane & t_prrep[pi];
-          lds_add(hist + t_proff[pi] + (rep * t_nlev[f] + cv[f] - 1) * t_nlev[g] + cv[g] - 1, w,
-                  hsc[0]);
-        }
+        const int4 tn = ptab[cat_pair(f, g, FM) + 1];
+        if (!(DLSA_CAT_ABLATE & 2) && g < F && cv[f] > 0 && cv[g] > 0)
+          lds_add(hist + tp.x + ((lane & tp.y) * tp.z + cv[f] - 1) * tp.w + cv[g] - 1, w, hsc[0]);
+        tp = tn;
       }
   }
 

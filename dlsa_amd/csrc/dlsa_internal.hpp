@@ -303,7 +303,8 @@ hipError_t launch_partition_scatter(const int32_t* pid, int64_t n, int K, int64_
 // Launchers (defined in the .hip files).
 hipError_t launch_cat_pass(const CatArgs& a, bool standardize, int n_chunks, hipStream_t s);
 size_t cat_lds_bytes(const CatArgs& a);  // dynamic LDS of the pass
-constexpr int kCatStaticLds = 4 * (5 * kCatMaxFactors + 2 * kCatMaxPairs);  // its tables
+constexpr int kCatStaticLds =  // its tables: factor and pair records, dummy offsets
+    16 * (kCatMaxFactors + 1) + 16 * (kCatMaxPairs + 1) + 4 * kCatMaxFactors;
 hipError_t launch_cat_presence(const CatArgs& a, int n_chunks, int32_t* counts, int32_t* bad,
                                double* colmax,
                                hipStream_t s);

@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round 5, run cr: categorical pass with the factor / pair records read one
+# step ahead of the histogram adds (product) vs the committed pass (catold):
+# bit-identity across builds, the categorical GPU tests, config-3 A/B.
+set -o pipefail
+OUT=gpurun_out/${TAG:-r05cr}; mkdir -p $OUT
+PYTHONPATH=. DLSA_LIB=var/libdlsa_hip_catold.so timeout -k 10 120 python -u tools/cat_xbuild.py $OUT/old.npz > $OUT/xb.log 2>&1 || exit $?
+PYTHONPATH=. timeout -k 10 120 python -u tools/cat_xbuild.py $OUT/new.npz >> $OUT/xb.log 2>&1 || exit $?
+python tools/cat_xbuild.py --compare $OUT/old.npz $OUT/new.npz | tee -a $OUT/xb.log || exit $?
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests/test_gpu_parity.py -k categorical > $OUT/pytest.log 2>&1 || exit $?
+run() {
+  DLSA_LIB=$2 timeout -k 10 200 python -u bench.py --config 3 --steps 5 --warmup 2 --no-cpu-baseline --no-parity > $OUT/tmp.json 2>> $OUT/err.log || return $?
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); k=d['kernels']['cat_pass_kernel']; print(json.dumps({'variant': sys.argv[2], 'ms_per_step': round(d['ms_per_step'],2), 'cat_ms_per_step': round(k['ms_per_step'],3), 'cat_avg_launch_ms': round(k['avg_launch_ms'],3)}))" $OUT/tmp.json "$1" | tee -a $OUT/sweep.jsonl
+}
+for r in 1 2; do
+  run readahead dlsa_amd/libdlsa_hip.so || exit $?
+  run old var/libdlsa_hip_catold.so || exit $?
+done
+cp $OUT/tmp.json $OUT/last_bench.json
