@@ -97,7 +97,8 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
   constexpr int NPM = FM * (FM - 1) / 2;
   __shared__ int4 ftab[kCatMaxFactors + 1];
   __shared__ int4 ptab[kCatMaxPairs + 1];
-  __shared__ int32_t t_doff[kCatMaxFactors];
+  __shared__ int4 dtab[kCatMaxFactors / 4];  // first dummy parameter of each factor
+  int32_t* t_doff = (int32_t*)dtab;
   for (int i = tid; i <= FM; i += NTHR)
     ftab[i] = i < F ? make_int4(a.nd_rep[i] - 1, a.nlev[i], a.nd_off[i], a.g_off[i])
                     : make_int4(0, 0, 0, 0);
@@ -172,9 +173,24 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
       else
         e0 = fma(xv[i], th[i], e0);
     }
+    // dummy effects: the gathers are unconditional (a baseline code reads a
+    // valid slot and adds +0), so they issue back to back and one wait covers
+    // them instead of one per factor
+    // (the offsets are read as 16-byte records, FM / 4 reads and one wait)
+    int4 dof[FM / 4];
 #pragma unroll
-    for (int f = 0; f < FM; ++f)
-      if (f < F && cv[f] > 0) e0 += th[t_doff[f] + cv[f] - 1];
+    for (int k = 0; k < FM / 4; ++k) dof[k] = dtab[k];
+    double de[FM];
+#pragma unroll
+    for (int f = 0; f < FM; ++f) {
+      const int4 d4 = dof[f / 4];
+      const int d = (f & 3) == 0 ? d4.x : (f & 3) == 1 ? d4.y : (f & 3) == 2 ? d4.z : d4.w;
+      const bool on = f < F && cv[f] > 0;
+      const double t = th[f < F ? d + (on ? cv[f] - 1 : 0) : 0];
+      de[f] = on ? t : 0.0;
+    }
+#pragma unroll
+    for (int f = 0; f < FM; ++f) e0 += de[f];
     const double e = e0 + e1;
     const double ea = exp(-fabs(e));
     const double inv = 1.0 / (1.0 + ea);

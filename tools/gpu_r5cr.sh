@@ -13,7 +13,7 @@ run() {
   python3 -c "import json,sys; d=json.load(open(sys.argv[1])); k=d['kernels']['cat_pass_kernel']; print(json.dumps({'variant': sys.argv[2], 'ms_per_step': round(d['ms_per_step'],2), 'cat_ms_per_step': round(k['ms_per_step'],3), 'cat_avg_launch_ms': round(k['avg_launch_ms'],3)}))" $OUT/tmp.json "$1" | tee -a $OUT/sweep.jsonl
 }
 for r in 1 2; do
-  run readahead dlsa_amd/libdlsa_hip.so || exit $?
+  run ${NEWTAG:-readahead} dlsa_amd/libdlsa_hip.so || exit $?
   run old var/libdlsa_hip_catold.so || exit $?
 done
 cp $OUT/tmp.json $OUT/last_bench.json
