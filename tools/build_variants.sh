@@ -16,6 +16,7 @@ for v in "$@"; do
     cat7) D=DLSA_CAT_ABLATE=7 ;;
     cat15) D=DLSA_CAT_ABLATE=15 ;;
     cat16) D=DLSA_CAT_ABLATE=16 ;;
+    cat8) D=DLSA_CAT_ABLATE=8 ;;
     solveprof) D=DLSA_SOLVE_PROFILE=1 ;;
     solveblk) D=DLSA_SOLVE_BLOCKED=1 ;;
     solversq1) D=DLSA_SOLVE_RSQ_STEPS=1 ;;
@@ -63,6 +64,7 @@ for v in "$@"; do
   case $v in
     oz*|ozs*) ONLY='["irls_oz.hip", "irls_oz_g2.hip"]' ;;
     solve*) ONLY='["newton_solve.hip"]' ;;
+    cat*) ONLY='["cat_pass.hip"]' ;;
     olswave|olsks2|olsks8|olsks12|olsks16) ONLY='["ols_stream.hip"]' ;;
     olsks2k) ONLY='["ols_stream.hip", "capi.hip"]' ;;
     wn*|wrow*) ONLY='["wide_pass.hip"]' ;;
