@@ -278,6 +278,12 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
     for (int w = 0; w < NW; ++w) s += red[w * NR + i];
     fin[i] = s;
   }
+  // the epilogue's per-entry lookups come from LDS: the factor / pair records
+  // and the grids (staged over theta, which the row loop no longer reads),
+  // not from the kernel arguments at a lane-dependent index (dependent memory
+  // round trips; 0.015 ms per launch, profiles/r05cf_cat_epilogue_ab.jsonl)
+  double* hsl = th;
+  for (int i = tid; i < kCatQMax + 2; i += NTHR) hsl[i] = hs[i];
   __syncthreads();
 
   // factor of dummy parameter index d (0-based among dummies)
@@ -285,17 +291,16 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
     int f = 0;
 #pragma unroll
     for (int g = 1; g < FM; ++g)
-      if (g < F && gi >= a.doff[g]) f = g;
-    lev = gi - a.doff[f];
+      if (g < F && gi >= t_doff[g]) f = g;
+    lev = gi - t_doff[f];
     return f;
   };
   // exact integer sums over the replicas, one rounding back to fp64
   auto nd_sum = [&](int f, int lev, int col) {
-    const int nl = a.nlev[f], R = a.nd_rep[f];
+    const int4 r = ftab[f];  // {R - 1, levels, nd offset, g offset}
     long long s = 0;
-    for (int rp = 0; rp < R; ++rp)
-      s += hist_at(hist, a.nd_off[f] + (rp * nl + lev) * a.nd_stride + col);
-    return (double)s / (col == 0 ? hs[0] : hs[1 + col]);
+    for (int rp = 0; rp <= r.x; ++rp) s += hist_at(hist, r.z + (rp * r.y + lev) * a.nd_stride + col);
+    return (double)s / (col == 0 ? hsl[0] : hsl[1 + col]);
   };
 
   // ---- epilogue: the partial slab in the dense pass's tile format ---------
@@ -323,11 +328,11 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
           if (fj == fi) {
             v = li == lj ? nd_sum(fi, li, 0) : 0.0;
           } else {  // fj < fi
-            const int pi = cat_pair(fj, fi, F);
-            const int nli = a.nlev[fi], nlj = a.nlev[fj], R = a.pr_rep[pi];
+            // {offset, R - 1, L_fj, L_fi} at the pair's row-loop position
+            const int4 r = ptab[cat_pair(fj, fi, FM)];
             long long s = 0;
-            for (int rp = 0; rp < R; ++rp) s += hist_at(hist, a.pr_off[pi] + (rp * nlj + lj) * nli + li);
-            v = (double)s / hs[0];
+            for (int rp = 0; rp <= r.y; ++rp) s += hist_at(hist, r.x + (rp * r.z + lj) * r.w + li);
+            v = (double)s / hsl[0];
           }
         }
       }
@@ -342,10 +347,10 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
     } else if (e < P) {
       int l;
       const int f = factor_of(e, l);
-      const int nl = a.nlev[f], R = a.nd_rep[f];
+      const int4 r = ftab[f];
       long long s = 0;
-      for (int rp = 0; rp < R; ++rp) s += hist_at(hist, a.g_off[f] + rp * nl + l);
-      v = (double)s / hs[1];
+      for (int rp = 0; rp <= r.x; ++rp) s += hist_at(hist, r.w + rp * r.y + l);
+      v = (double)s / hsl[1];
     }
     a.slab_g[(int64_t)chunk * PP + e] = v;
   }

@@ -15,7 +15,7 @@ run() {
   python3 -c "import json,sys; d=json.load(open(sys.argv[1])); k=d['kernels']['cat_pass_kernel']; print(json.dumps({'variant': sys.argv[2], 'ms_per_step': round(d['ms_per_step'],2), 'launches': k['launches_per_step'], 'cat_ms_per_step': round(k['ms_per_step'],3), 'cat_avg_launch_ms': round(k['avg_launch_ms'],3)}))" $OUT/tmp.json "$1" | tee -a $OUT/sweep.jsonl
 }
 for r in 1 2; do
-  run exact dlsa_amd/libdlsa_hip.so || exit $?
+  run ${NEWTAG:-exact} dlsa_amd/libdlsa_hip.so || exit $?
   run head var/libdlsa_hip_cathead.so || exit $?
 done
-for v in cat16 cat1 cat8 cat7; do run $v var/libdlsa_hip_$v.so || exit $?; done
+[ -n "$ABL" ] && for v in $ABL; do run $v var/libdlsa_hip_$v.so || exit $?; done; true
