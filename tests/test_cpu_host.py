@@ -517,3 +517,20 @@ def test_sharded_describe_gloo_equals_one_rank():
     for i in range(1, 5):
         for j in range(1, 4):
             assert abs(float(got[i, j]) - float(one[i, j])) <= 1e-13 * max(1.0, abs(float(one[i, j])))
+
+
+def test_pmc_traffic_records_match_bench_kernel_keys():
+    """bench.py fills roofline.traffic only when the PMC record's kernel_key is
+    the key it computes for the config's dominant kernel (bench.py pmc_key):
+    a record under another key leaves traffic null without an error."""
+    import json
+    import os
+    root = os.path.join(os.path.dirname(__file__), "..")
+    rec = json.load(open(os.path.join(root, "profiles", "pmc_traffic.json")))
+    src = open(os.path.join(root, "bench.py")).read()
+    # (config 3's p counts the numeric and dummy columns, without the intercept)
+    want = {"config2": ("irls_coop<bf16>", 100), "config3": ("cat_pass_kernel", 181),
+            "config4": ("ols_stream", 64), "config5": ("wide_fused_bf16", 500)}
+    for cfg, (key, p) in want.items():
+        assert f'pmc_key = "{key}"' in src, key
+        assert rec[cfg]["kernel_key"] == key and rec[cfg]["p"] == p, (cfg, rec[cfg])
