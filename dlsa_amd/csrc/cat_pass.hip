@@ -238,15 +238,19 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
       }
       tf = tn;
     }
-    int4 tp = ptab[0];
+    // pairs: one add each, so the records are read two ahead (one ahead,
+    // every wait would drain all but the last add)
+    int4 tp = ptab[0], tp1 = ptab[1];
 #pragma unroll
     for (int f = 0; f < FM; ++f)
 #pragma unroll
       for (int g = f + 1; g < FM; ++g) {
-        const int4 tn = ptab[cat_pair(f, g, FM) + 1];
+        const int pn = cat_pair(f, g, FM) + 2;
+        const int4 tn = ptab[pn <= kCatMaxPairs ? pn : kCatMaxPairs];
         if (!(DLSA_CAT_ABLATE & 2) && g < F && cv[f] > 0 && cv[g] > 0)
           lds_add(hist + tp.x + ((lane & tp.y) * tp.z + cv[f] - 1) * tp.w + cv[g] - 1, w, hsc[0]);
-        tp = tn;
+        tp = tp1;
+        tp1 = tn;
       }
   }
 
