@@ -2,7 +2,9 @@
 # Round 5, run ce: the exact-bucket categorical kernel (EX: compile-time column
 # count and intercept) vs the previous pass (cathead): bit-identity across
 # builds, the categorical GPU tests, config-3 A/B; then the ablations of
-# gpu_r5ca.sh on the previous pass.
+# gpu_r5ca.sh on the previous pass (ABL="cat16 cat1 ..."; tools/build_variants.sh).
+# Needs var/libdlsa_hip_cathead.so: a copy of the in-tree library built
+# before the change (cp dlsa_amd/libdlsa_hip.so var/libdlsa_hip_cathead.so).
 set -o pipefail
 OUT=gpurun_out/${TAG:-r05ce}; mkdir -p $OUT
 PYTHONPATH=. DLSA_LIB=var/libdlsa_hip_cathead.so timeout -k 10 120 python -u tools/cat_xbuild.py $OUT/old.npz > $OUT/xb.log 2>&1 || exit $?
