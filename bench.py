@@ -612,6 +612,27 @@ def main():
         out["parity_rel"] = rel
         out["parity_sample"] = (f"partitions {smp} of rank 0 vs the numpy oracle (tol 1e-12): "
                                 "max |diff| / max |ref| over theta and Sig_inv")
+    if rank == 0 and not args.no_parity:
+        # every partition of rank 0 (not a sample): Sig_inv per entry against an
+        # independent fp64 library-GEMM evaluation of models.py:114,130 at the
+        # returned theta_k, and the WLSE of those independent sums
+        # (oracle/device_check.py; after the timed region)
+        from oracle.device_check import check_all_partitions
+        torch.cuda.synchronize()
+        t_ck = time.perf_counter()
+        design = None
+        if codes_layout:
+            from dlsa_amd.models import expand_categorical
+            design = lambda a, b: expand_categorical(X[a:b], codes[a:b], levels)  # noqa: E731
+        r = check_all_partitions(fit, X, y, family=family, design=design)
+        out["sig_inv_all_partitions"] = {
+            k: r[k] for k in ("partitions", "max_elem_err", "worst_partition",
+                              "sig_inv_theta_rel", "wlse_rel")}
+        out["sig_inv_all_partitions"]["note"] = (
+            "every partition of rank 0: max_ij |Sig_inv_ij - H_ij| / sqrt(H_ii H_jj) with "
+            "H = X_k^T diag(w) X_k at the returned theta_k by torch fp64 GEMMs (an independent "
+            "library path); wlse_rel = WLSE of the independent sums vs the product's sums; "
+            f"{time.perf_counter() - t_ck:.1f} s, after the timed region")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         workers, cinfo = host_cores()      # every core this process may use
         if args.config == 5:

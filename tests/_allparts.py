@@ -1,0 +1,32 @@
+"""Shared checker of the full-size GPU tests: every partition's Sig_inv
+against oracle/device_check.py's independent library-GEMM evaluation, and the
+combine + DBIC selection on those independent sums (test infrastructure)."""
+
+import numpy as np
+
+import oracle as O
+from oracle.device_check import check_all_partitions
+
+
+def all_partitions_independent(fit, X, y, n, sel, design=None, family="logistic"):
+    """EVERY partition's Sig_inv against an independent evaluation of
+    models.py:114,130 at the returned theta_k (torch fp64 library GEMMs on the
+    device, oracle/device_check.py), per entry < 1e-10; Sig_invMcoef too; then
+    WLSE and the DBIC support from the independent sums (dlsa.py:30-49,
+    77-86) must equal the product's."""
+    from dlsa_amd.dlsa import dlsa
+
+    r = check_all_partitions(fit, X, y, family=family, design=design)
+    print(f"all-partition check: K={r['partitions']} max per-entry {r['max_elem_err']:.3e} "
+          f"(partition {r['worst_partition']}), Sig_invMcoef {r['sig_inv_theta_rel']:.3e}, "
+          f"WLSE {r['wlse_rel']:.3e}")
+    assert r["max_elem_err"] < 1e-10, r["worst_partition"]
+    assert r["sig_inv_theta_rel"] < 1e-10
+    assert r["wlse_rel"] < 1e-10
+    if family == "logistic":
+        sup = np.nonzero(sel["beta_byBIC"].to_numpy())[0].tolist()
+        sel_i = dlsa(r["Ssum"], r["wlse"], n, fit_intercept=fit.fit_intercept)
+        assert np.nonzero(sel_i["beta_byBIC"].to_numpy())[0].tolist() == sup
+        _, b_i = O.dlsa(r["Ssum"], r["wlse"], n, fit_intercept=fit.fit_intercept)
+        assert np.nonzero(b_i)[0].tolist() == sup
+    return r

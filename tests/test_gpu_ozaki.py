@@ -419,5 +419,7 @@ def test_ozaki_polish_pass_per_entry(torch_cuda, M, monkeypatch, kind):
     off = np.array([0, 7000, 15000, 24000])
     oz, f64 = _pair(M, monkeypatch, X, y, off, max_iter=4, rows_per_chunk=2048)
     assert oz.stats["polish_partitions"] >= 1, oz.stats
+    print(kind, {k: oz.stats[k] for k in ("passes_oz", "oz_stale_partitions",
+                                          "polish_partitions", "passes_fp64")})
     assert _rel(oz.theta.cpu(), f64.theta.cpu()) < 1e-10
     assert _elem(oz.sig_inv.cpu(), f64.sig_inv.cpu()) < 1e-10

@@ -519,6 +519,8 @@ def test_config5_shape_sampled_partitions(torch_cuda, M):
     sup = np.nonzero(sel["beta_byBIC"].to_numpy())[0].tolist()
     assert sup == np.nonzero(b_bic)[0].tolist()
     assert set(range(200)) <= set(sup)  # the 0.4 p true nonzeros are all kept
+    from _allparts import all_partitions_independent
+    all_partitions_independent(fit, X, y, K * nk, sel)  # all 32 partitions, per entry
 
 
 # ---------------------------------------------------------------------------

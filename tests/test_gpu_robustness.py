@@ -232,12 +232,13 @@ def test_categorical_inf_fails_only_its_partition(torch_cuda, M):
     assert np.isfinite(buf).all()
 
 
-@pytest.mark.parametrize("p", [8, 200])
+@pytest.mark.parametrize("p", [8, 16, 100, 200])
 def test_huge_magnitude_fails_only_its_partition(torch_cuda, M, p):
     """A value of 2^1010 in partition 1 (beyond the int8 digit grid's EMAX:
     its digits would wrap to a finite, wrong Gram): partition 1 must end in a
     failure status -- never status ok with a finite Sig_inv -- and the other
-    partitions match the oracle (fused P <= 192 and wide P > 192 paths)."""
+    partitions match the oracle (fused P <= 192 -- p = 16 and 100 are on the
+    int8 exact pass's shapes, P >= 12 -- and wide P > 192 paths)."""
     rng = np.random.default_rng(5 + p)
     n_k, K = 3000, 3
     X = rng.normal(size=(n_k * K, p)) * 0.3

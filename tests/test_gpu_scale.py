@@ -16,6 +16,7 @@ import numpy as np
 import pytest
 
 import oracle as O
+from _allparts import all_partitions_independent
 
 pytestmark = pytest.mark.gpu
 
@@ -91,6 +92,7 @@ def test_config2_full_K1024(torch_cuda, M):
     _, b_bic = O.dlsa(Ssum, comb["beta_byOLS"].to_numpy(), n)
     assert np.nonzero(sel["beta_byBIC"].to_numpy())[0].tolist() == np.nonzero(b_bic)[0].tolist()
     assert set(range(40)) <= set(np.nonzero(b_bic)[0].tolist())  # the 0.4 p true nonzeros
+    all_partitions_independent(fit, X, y, n, sel)
 
 
 def test_config3_partition_size(torch_cuda, M):
@@ -121,6 +123,14 @@ def test_config3_partition_size(torch_cuda, M):
         o = O.logistic_fit(Xh[a:b], yh[a:b])  # intercept column already in Xh
         assert _rel(fit.theta[k].cpu(), o["coef"]) < REL
         assert _rel(fit.sig_inv[k].cpu(), o["Sig_inv"]) < REL
+    del Xh
+    # every partition per entry, on the device-expanded dense design (the
+    # check adds the intercept column itself), and the selection on those sums
+    from dlsa_amd.dlsa import dlsa, dlsa_mapred
+    comb = dlsa_mapred(fit)
+    sel = dlsa(comb.iloc[:, 2:].to_numpy(), comb["beta_byOLS"], n, fit_intercept=True)
+    Xe = Xd[:, 1:]
+    all_partitions_independent(fit, Xn, y, n, sel, design=lambda a, b: Xe[a:b])
 
 
 def test_config3_reference_partition_policy(torch_cuda, M):
@@ -156,6 +166,13 @@ def test_config3_reference_partition_policy(torch_cuda, M):
     o = O.logistic_fit(Xh, yh)  # intercept column already in Xh
     assert _rel(fit.theta[0].cpu(), o["coef"]) < REL
     assert _rel(fit.sig_inv[0].cpu(), o["Sig_inv"]) < REL
+    # both 1e6-row partitions per entry (dense rows expanded per partition)
+    from dlsa_amd.dlsa import dlsa, dlsa_mapred
+    comb = dlsa_mapred(fit)
+    sel = dlsa(comb.iloc[:, 2:].to_numpy(), comb["beta_byOLS"], n, fit_intercept=True)
+    all_partitions_independent(fit, Xn, y, n, sel,
+                               design=lambda a, b: M.expand_categorical(Xn[a:b], codes[a:b],
+                                                                        levels))
 
 
 def test_config4_partition_size(torch_cuda, M):
@@ -185,6 +202,7 @@ def test_config4_partition_size(torch_cuda, M):
         o = O.ols_fit(X[a:b].cpu().numpy(), y[a:b].cpu().numpy())
         assert _rel(fit.theta[k].cpu(), o["coef"]) < REL
         assert _rel(fit.sig_inv[k].cpu(), o["Sig_inv"]) < 1e-12
+    all_partitions_independent(fit, X, y, n, None, family="ols")
 
 
 def test_wide_skewed_partitions_level_plans(torch_cuda, M):

@@ -17,6 +17,10 @@ for v in "$@"; do
     cat15) D=DLSA_CAT_ABLATE=15 ;;
     cat16) D=DLSA_CAT_ABLATE=16 ;;
     cat8) D=DLSA_CAT_ABLATE=8 ;;
+    catpf0) D=DLSA_CAT_PF=0 ;;
+    catpf1) D=DLSA_CAT_PF=1 ;;
+    cat32) D="DLSA_CAT_PF=0 -DDLSA_CAT_ABLATE=32" ;;
+    catpf32) D=DLSA_CAT_ABLATE=32 ;;
     solveprof) D=DLSA_SOLVE_PROFILE=1 ;;
     solveblk) D=DLSA_SOLVE_BLOCKED=1 ;;
     solversq1) D=DLSA_SOLVE_RSQ_STEPS=1 ;;

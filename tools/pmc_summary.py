@@ -12,7 +12,11 @@ grid stream all n rows), so bench.py can scale it to the rows per launch of
 whatever launch mix it measured -- traffic and the algorithmic bytes then
 describe the same launches.
 
-Usage: python tools/pmc_summary.py <tag> <out-prefix> <config> <n> <p> <kernel-key> <regex>
+Usage: python tools/pmc_summary.py <tag> <out-prefix> <config> <n> <p> <kernel-key> <regex> [<run-prefix>]
+
+<run-prefix> keeps only the run directories whose name starts with it (a
+tools/gpu.sh / closing_run.sh tag holds every config's passes: pmc_c2_p1,
+pmc_c2_p2, pmc_c3_p1, ...; use e.g. "pmc_c2_").
 """
 import csv
 import glob
@@ -22,12 +26,15 @@ import re
 import sys
 
 tag, prefix, config, n, p, key, rx = sys.argv[1:8]
+run_prefix = sys.argv[8] if len(sys.argv) > 8 else ""
 pattern = re.compile(rx)
 root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 base = os.path.join(root, "gpurun_out", tag)
 rows = []
 for f in sorted(glob.glob(os.path.join(base, "**", "*counter_collection.csv"), recursive=True)):
     i = os.path.relpath(f, base).split(os.sep)[0]  # one counter group per run directory
+    if not i.startswith(run_prefix):
+        continue
     for r in csv.DictReader(open(f)):
         if any(t in r["Kernel_Name"] for t in ("irls_", "wide_", "cat_", "part_", "ols_")):
             rows.append({"pass": i, "dispatch": r["Dispatch_Id"],
