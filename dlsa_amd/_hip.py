@@ -67,6 +67,7 @@ class FitStats(ctypes.Structure):
         ("polish_partitions", ctypes.c_int32),
         ("passes_oz", ctypes.c_int32),
         ("oz_fallbacks", ctypes.c_int32),
+        ("oz_stale_partitions", ctypes.c_int32),
     ]
 
     def as_dict(self):

@@ -223,12 +223,14 @@ static Layout make_layout(const Plan& pl, int K) {
   L.off_slabH = take(8LL * std::max(pl.n_chunks, 1) * pl.T * 256);
   L.off_slabg = take(8LL * std::max(pl.n_chunks, 1) * pl.PP);
   L.off_slabll = take(8LL * std::max(pl.n_chunks, 1));
-  L.off_phase = take(4LL * K);
+  // the counters and the phases are adjacent (counters first, as in the
+  // pinned staging): one readback per iteration
+  L.off_counters = take(16 + 4LL * K);
+  L.off_phase = L.off_counters + 16;
   L.off_bt = take(4LL * K);
   L.off_llprev = take(8LL * K);
   L.off_thprev = take(8LL * K * pl.P);
   L.off_dprev = take(8LL * K * pl.P);
-  L.off_counters = take(16);
   L.off_dmprev = take(8LL * K);
   L.off_stall = take(4LL * K);
   L.off_colmax = take(4LL * std::max(pl.n_chunks, 1) * pl.PP);
@@ -327,12 +329,14 @@ static WideLayout make_wide_layout(const std::vector<WidePlans>& plans, int K, i
   L.off_slabgz = take(8 * ng * PP);
   L.off_slabllz = take(8 * ng);
   L.off_H = take(8LL * K * PP * PP);
-  L.off_phase = take(4LL * K);
+  // the counters and the phases are adjacent (counters first, as in the
+  // pinned staging): one readback per iteration
+  L.off_counters = take(16 + 4LL * K);
+  L.off_phase = L.off_counters + 16;
   L.off_bt = take(4LL * K);
   L.off_llprev = take(8LL * K);
   L.off_thprev = take(8LL * K * P);
   L.off_dprev = take(8LL * K * P);
-  L.off_counters = take(16);
   L.off_dmprev = take(8LL * K);
   L.off_stall = take(4LL * K);
   L.off_zmax = take(4 * nr * PP);
@@ -746,9 +750,10 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
       DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
       DLSA_HIP_TRY(launch_level_reset(K, P, start_phase, d_phase, status, d_llprev, d_bt, theta,
                                       d_cnt, stream));
-      DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, stream));
+      DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16 + 4LL * K, hipMemcpyDeviceToHost, stream));
+    } else {
+      DLSA_HIP_TRY(hipMemcpyAsync(h_phase, d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
     }
-    DLSA_HIP_TRY(hipMemcpyAsync(h_phase, d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
     DLSA_HIP_TRY(hipStreamSynchronize(stream));
     if (lvl > 0)
       for (int ph = 0; ph < kRunPhases; ++ph) n_running[ph] = h_cnt[ph];
@@ -779,8 +784,8 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
       DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
       DLSA_HIP_TRY(timed(&g_stats.ms_solve,
                          [&] { return launch_wide_newton(sa, wa, d_rcb, d_gcb, d_H, K, stream); }));
-      DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, stream));
-      DLSA_HIP_TRY(hipMemcpyAsync(h_phase, d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
+      // counters + phases in one copy (adjacent on both sides)
+      DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16 + 4LL * K, hipMemcpyDeviceToHost, stream));
       DLSA_HIP_TRY(hipStreamSynchronize(stream));
       for (int ph = 0; ph < kRunPhases; ++ph) n_running[ph] = h_cnt[ph];
       if (getenv("DLSA_TRACE"))
@@ -1012,7 +1017,7 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
   const bool standardize = center != nullptr;
   StreamTimer timed{stream, opt.record_timing != 0};
 
-  int32_t* h_cnt = pinned_staging(4 + (size_t)K);
+  int32_t* h_cnt = pinned_staging(4 + 2 * (size_t)K);
   if (!h_cnt) {
     set_error("pinned host staging allocation failed");
     return DLSA_E_HIP;
@@ -1020,6 +1025,7 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
 
   const bool trace = getenv("DLSA_TRACE") != nullptr;
   int32_t* h_phase = h_cnt + 4;  // [K] phases (pinned: no staging copy per iteration)
+  int32_t* h_route = h_phase + K;  // [K] phases with stale partitions marked (one launch)
   // exact passes on the int8 matrix cores (irls_oz_impl.hpp) unless DLSA_EXACT_FP64:
   // the first full-data bf16 pass records, per chunk and feature, max |x|; the
   // bf16 passes that follow an iteration with a partition near the switch
@@ -1035,13 +1041,16 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
   bool colmax_ready = false;
   bool near_switch = false;  // counters[3] of the last solve
   // per partition: the last approximate pass that processed it recorded max |z|
-  // (so its exact pass starts from a record one small step away); an exact
-  // pass with any partition lacking one runs on the fp64 MFMA instead: without
-  // a fresh record the digit exponents fall back to max |x| / 2, which a
-  // column with large |x| at w ~ 0 (an outlier row) turns into ~1e-5 per-entry
-  // errors (tests/test_gpu_ozaki.py::test_ozaki_polish_pass_per_entry)
+  // (so its exact pass starts from a record one small step away); a partition
+  // lacking one runs its exact pass on the fp64 MFMA instead (a second launch
+  // beside the int8 one, PHASE_F64_STALE): without a fresh record the digit
+  // exponents fall back to max |x| / 2, which a column with large |x| at w ~ 0
+  // (an outlier row) turns into ~1e-5 per-entry errors
+  // (tests/test_gpu_ozaki.py::test_ozaki_polish_pass_per_entry)
   std::vector<char> zfresh((size_t)K, 0);
-  // DLSA_OZ_ZREC=0 (A/B only): no max |z| records, every exponent from max |x| / 2
+  // DLSA_OZ_ZREC=0 (knob builds, A/B only): no max |z| records, so no partition
+  // is ever fresh and every exact pass runs on the fp64 MFMA (it no longer
+  // measures round 3's "every exponent from max |x| / 2" int8 pass)
   const bool zrec = !(env_knob("DLSA_OZ_ZREC") && atoi(env_knob("DLSA_OZ_ZREC")) == 0);
   if (use_oz) {
     DLSA_HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)d_zcolmax, 0x7F800000u,
@@ -1059,10 +1068,22 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
     const int prec = f64 ? PREC_F64 : (ph == PHASE_F32X ? PREC_F32 : approx_prec);
     pa.want_phase = ph;
     const bool wave = f64 && q.NT <= kWaveMaxNT;
-    bool fresh = true;
+    int n_fresh = 0, n_stale = 0;
     if (f64)
-      for (int k = 0; k < K; ++k) fresh = fresh && (hph[k] != PHASE_F64 || zfresh[k]);
-    const bool oz = wave && use_oz && colmax_ready && full && fresh;
+      for (int k = 0; k < K; ++k)
+        if (hph[k] == PHASE_F64) (zfresh[k] ? n_fresh : n_stale)++;
+    const bool oz = wave && use_oz && colmax_ready && full && n_fresh > 0;
+    // int8 for the fresh partitions, fp64 MFMA for the stale ones: the stale
+    // ones are marked PHASE_F64_STALE on the device for the int8 launch (which
+    // skips them), then passed by the per-wave fp64 kernel, then restored
+    const bool split = oz && n_stale > 0;
+    if (split) {
+      for (int k = 0; k < K; ++k)
+        h_route[k] = (hph[k] == PHASE_F64 && !zfresh[k]) ? PHASE_F64_STALE : hph[k];
+      hipError_t e = hipMemcpyAsync(d_phase, h_route, 4LL * K, hipMemcpyHostToDevice, stream);
+      if (e != hipSuccess) return e;
+      g_stats.oz_stale_partitions += n_stale;
+    }
     // digit-scale records of a full-data bf16 pass: max |x| on the first,
     // max |z| near the switch
     const bool rec_x = use_oz && full && ph == PHASE_F32 && !colmax_ready;
@@ -1076,13 +1097,24 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
       pc.colmax = (oz || rec_x) ? d_colmax : nullptr;
       pc.zcolmax = (oz || rec_z) ? d_zcolmax : nullptr;
       pc.theta_rec = d_threc;
-      if (oz) return launch_irls_oz(pc, q.NT, standardize, family, q.n_chunks, stream);
-      // OLS (one pass at theta = 0): X streamed into registers, no LDS ring
-      if (f64 && family == FAMILY_GAUSSIAN && ols_stream_applies(q.NT))
+      if (oz) {
+        hipError_t eo = launch_irls_oz(pc, q.NT, standardize, family, q.n_chunks, stream);
+        if (eo != hipSuccess || !split) return eo;
+        PassArgs ps = pa;  // the stale partitions on the fp64 MFMA
+        ps.want_phase = PHASE_F64_STALE;
+        return launch_irls_wave(ps, q.NT, standardize, family, q.n_chunks, stream);
+      }
+      // OLS (one pass at theta = 0): X streamed into registers, no LDS ring.
+      // Its buffer range and row offsets are 32-bit: a caller's rows_per_chunk
+      // of >= 2^31 bytes per chunk takes the per-wave kernel instead
+      if (f64 && family == FAMILY_GAUSSIAN && ols_stream_applies(q.NT) &&
+          (int64_t)q.max_chunk_rows * p * 8 < (1LL << 31))
         return launch_ols_stream(pc, q.NT, standardize, q.n_chunks, stream);
       if (wave) return launch_irls_wave(pc, q.NT, standardize, family, q.n_chunks, stream);
       return launch_irls_coop(pc, q.NT, prec, standardize, family, q.n_chunks, stream);
     });
+    if (split && e == hipSuccess)  // hph is the pinned readback, unchanged until the next sync
+      e = hipMemcpyAsync(d_phase, hph, 4LL * K, hipMemcpyHostToDevice, stream);
     if (rec_x) colmax_ready = true;
     if (!f64)  // this pass's partitions moved on from their records unless it took one
       for (int k = 0; k < K; ++k)
@@ -1108,9 +1140,10 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
       DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
       DLSA_HIP_TRY(launch_level_reset(K, P, start_phase, d_phase, status, d_llprev, d_bt, theta,
                                       d_cnt, stream));
-      DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, stream));
+      DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16 + 4LL * K, hipMemcpyDeviceToHost, stream));
+    } else {
+      DLSA_HIP_TRY(hipMemcpyAsync(h_phase, d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
     }
-    DLSA_HIP_TRY(hipMemcpyAsync(h_phase, d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
     DLSA_HIP_TRY(hipStreamSynchronize(stream));
     if (lvl > 0)
       for (int ph = 0; ph < kRunPhases; ++ph) n_running[ph] = h_cnt[ph];
@@ -1132,8 +1165,8 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
       }
       DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
       DLSA_HIP_TRY(timed(&g_stats.ms_solve, [&] { return launch_newton_solve(sa, K, stream); }));
-      DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, stream));
-      DLSA_HIP_TRY(hipMemcpyAsync(h_phase, d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
+      // counters + phases in one copy (adjacent on both sides)
+      DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16 + 4LL * K, hipMemcpyDeviceToHost, stream));
       DLSA_HIP_TRY(hipStreamSynchronize(stream));
       for (int ph = 0; ph < kRunPhases; ++ph) n_running[ph] = h_cnt[ph];
       near_switch = final_level && h_cnt[3] > 0;
@@ -1172,27 +1205,40 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
 }
 
 // ---- categorical-code fit (cat_pass.hip) ---------------------------------
+// level slots x replicas per factor of the numeric x dummy histograms before
+// the LDS budget shrinks them (A/B builds: DLSA_CAT_ND_CAP)
+#ifndef DLSA_CAT_ND_CAP
+#define DLSA_CAT_ND_CAP 128
+#endif
 // LDS layout of the histograms: replicas so that a frequent level does not
 // serialise the lanes of a wave on one address (nd: <= 128 slots per factor,
 // pairs: <= 512 cells), shrunk until the workgroup fits 160 KB.
 static bool cat_layout(CatArgs& a, const int32_t* levels) {
   const int Qw = (a.q + 1) | 1;
   a.nd_stride = Qw;
-  int nd_cap = 128, pr_cap = 512;
+  // the exact-bucket kernel folds the intercept row into the histograms of the
+  // factor with the most levels (its baseline is the rarest: fewest extra adds)
+  a.fold = -1;
+  if (cat_exact_bucket(a))
+    for (int f = 0; f < a.F; ++f)
+      if (a.fold < 0 || levels[f] > levels[a.fold]) a.fold = f;
+  int nd_cap = DLSA_CAT_ND_CAP, pr_cap = 512;
   for (int attempt = 0; attempt < 12; ++attempt) {
     int64_t o = 0;
     for (int f = 0; f < a.F; ++f) {
       const int nl = levels[f] - 1;
+      const int ns = nl + (f == a.fold ? 1 : 0);  // level slots per replica
       int R = 1;
-      while (R < 16 && nl * R * 2 <= nd_cap) R *= 2;
+      while (R < 16 && ns * R * 2 <= nd_cap) R *= 2;
       a.nlev[f] = nl;
+      a.nd_lev[f] = ns;
       a.nd_rep[f] = R;
       a.nd_off[f] = (int32_t)o;
-      o += (int64_t)R * nl * Qw;
+      o += (int64_t)R * ns * Qw;
     }
     for (int f = 0; f < a.F; ++f) {
       a.g_off[f] = (int32_t)o;
-      o += (int64_t)a.nd_rep[f] * a.nlev[f];
+      o += (int64_t)a.nd_rep[f] * a.nd_lev[f];
     }
     for (int f = 0; f < a.F; ++f)
       for (int g = f + 1; g < a.F; ++g) {
@@ -1404,7 +1450,14 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
   // level presence over all rows: partitions missing a level -> zero frame;
   // invalid codes fail the call.  The same pass takes max |x_i| per column for
   // the fixed-point grids of the histograms (cat_pass.hip).
-  std::vector<int32_t> h_phase(K, 0), h_badp(K, 0);
+  // counters + phases in pinned staging (h_phase = h_cnt + 4, like d_cnt / d_phase)
+  int32_t* h_cnt = pinned_staging(4 + (size_t)K);
+  if (!h_cnt) {
+    set_error("pinned host staging allocation failed");
+    return DLSA_E_HIP;
+  }
+  int32_t* h_phase = h_cnt + 4;
+  std::vector<int32_t> h_badp(K, 0);
   std::vector<double> h_colmax((size_t)kCatQMax * std::max(pl.n_chunks, 1), 0.0);
   DLSA_HIP_TRY(upload(pl));
   DLSA_HIP_TRY(launch_cat_presence(ca, pl.n_chunks, d_counts, d_bad, d_colmax, stream));
@@ -1415,7 +1468,7 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
     DLSA_HIP_TRY(launch_cat_mark(ca, d_pcb, d_counts, d_bad, K, d_phase, status, d_badp, stream));
     DLSA_HIP_TRY(hipMemcpyAsync(h_badp.data(), d_badp, 4LL * K, hipMemcpyDeviceToHost, stream));
   }
-  DLSA_HIP_TRY(hipMemcpyAsync(h_phase.data(), d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
+  DLSA_HIP_TRY(hipMemcpyAsync(h_phase, d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
   DLSA_HIP_TRY(hipStreamSynchronize(stream));
   std::vector<double> h_hs;  // the grids (alive until the fit's next stream sync)
   {
@@ -1491,11 +1544,6 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
 
   const bool standardize = center != nullptr;
   StreamTimer timed{stream, opt.record_timing != 0};
-  int32_t* h_cnt = pinned_staging(4 + (size_t)K);
-  if (!h_cnt) {
-    set_error("pinned host staging allocation failed");
-    return DLSA_E_HIP;
-  }
   const bool trace = getenv("DLSA_TRACE") != nullptr;
 
   int it = 0;
@@ -1508,9 +1556,7 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
       DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
       DLSA_HIP_TRY(launch_level_reset(K, P, PHASE_F64, d_phase, status, d_llprev, d_bt, theta,
                                       d_cnt, stream));
-      DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, stream));
-      DLSA_HIP_TRY(hipMemcpyAsync(h_phase.data(), d_phase, 4LL * K, hipMemcpyDeviceToHost,
-                                  stream));
+      DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16 + 4LL * K, hipMemcpyDeviceToHost, stream));
       DLSA_HIP_TRY(hipStreamSynchronize(stream));
       n_running = h_cnt[0] + h_cnt[1] + h_cnt[2];
     }
@@ -1523,12 +1569,10 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
       DLSA_HIP_TRY(timed(&g_stats.ms_pass_fp64,
                          [&] { return launch_cat_pass(ca, standardize, qn.n_chunks, stream); }));
       g_stats.passes_fp64++;
-      g_stats.rows_fp64 += phase_rows(part_rows, h_phase.data(), PHASE_F64);
+      g_stats.rows_fp64 += phase_rows(part_rows, h_phase, PHASE_F64);
       DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
       DLSA_HIP_TRY(timed(&g_stats.ms_solve, [&] { return launch_newton_solve(sa, K, stream); }));
-      DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, stream));
-      DLSA_HIP_TRY(hipMemcpyAsync(h_phase.data(), d_phase, 4LL * K, hipMemcpyDeviceToHost,
-                                  stream));
+      DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16 + 4LL * K, hipMemcpyDeviceToHost, stream));
       DLSA_HIP_TRY(hipStreamSynchronize(stream));
       n_running = h_cnt[0] + h_cnt[1] + h_cnt[2];
       int nr[kRunPhases] = {h_cnt[0], h_cnt[1], h_cnt[2]};
@@ -1543,7 +1587,7 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
     DLSA_HIP_TRY(timed(&g_stats.ms_pass_fp64,
                        [&] { return launch_cat_pass(ca, standardize, pl.n_chunks, stream); }));
     g_stats.passes_fp64++;
-    g_stats.rows_fp64 += phase_rows(plan_part_rows(pl, K), h_phase.data(), PHASE_F64);
+    g_stats.rows_fp64 += phase_rows(plan_part_rows(pl, K), h_phase, PHASE_F64);
     g_stats.polish_partitions = n_running;
     sa.eval_only = 1;
     sa.subsample = 0;

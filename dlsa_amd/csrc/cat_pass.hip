@@ -42,9 +42,16 @@
 
 // Profiling-only ablation bits (tools/build_variants.sh cat*; product build 0):
 // 1 no numeric x dummy histogram adds, 2 no pair adds, 4 no gradient adds,
-// 8 no numeric register block, 16 no slab-epilogue lookups.
+// 8 no numeric register block, 16 no slab-epilogue lookups, 32 every row's
+// loads from the chunk's first 1024 rows (cache-resident: the HBM latency
+// and bytes removed).
 #ifndef DLSA_CAT_ABLATE
 #define DLSA_CAT_ABLATE 0
+#endif
+// Next row's loads issued under the current row's atomics (1) or at the end
+// of the iteration (0, A/B)
+#ifndef DLSA_CAT_PF
+#define DLSA_CAT_PF 1
 #endif
 
 namespace dlsa {
@@ -56,10 +63,11 @@ namespace dlsa {
 // integer -- an FMA and a 64-bit integer subtraction instead of the emulated
 // f64 -> i64 conversion (7 VALU ops, 5 of them fp64).  The grids (capi.hip
 // fit_categorical) bound every term by 2^50.
-__device__ __forceinline__ void lds_add(unsigned long long* p, double v, double scale) {
+__device__ __forceinline__ unsigned long long fx_term(double v, double scale) {
   const double t = fma(v, scale, 6755399441055744.0);  // 1.5 * 2^52
-  const unsigned long long u =
-      (unsigned long long)__double_as_longlong(t) - 0x4338000000000000ull;
+  return (unsigned long long)__double_as_longlong(t) - 0x4338000000000000ull;
+}
+__device__ __forceinline__ void lds_add_u(unsigned long long* p, unsigned long long u) {
   __hip_atomic_fetch_add(p, u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ long long hist_at(const unsigned long long* h, int i) {
@@ -79,15 +87,22 @@ template <int QN, int FM, int NTHR, bool STD, bool EX>
 __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   constexpr int NW = NTHR / 64;
-  constexpr int NTRI = QN * (QN + 1) / 2;
-  constexpr int NR = NTRI + QN + 1;  // reduced register values: H block, gradient, ll
+  // EX: the intercept row of the dense block (sum w, sum w x_i) and the
+  // intercept gradient (sum r) come from the fold factor's histograms, which
+  // also take its baseline level -- every row lands in exactly one of its
+  // levels -- so the register block holds the numeric columns only (-22 VGPRs:
+  // room for the next row's loads in flight)
+  constexpr int Q0 = EX ? 1 : 0;     // first register-block column
+  constexpr int NQ = QN - Q0;
+  constexpr int NTRI = NQ * (NQ + 1) / 2;
+  constexpr int NR = NTRI + NQ + 1;  // reduced register values: H block, gradient, ll
   const int chunk = blockIdx.x;
   const int part = a.chunk_part[chunk];
   if (a.phase[part] != a.want_phase) return;  // workgroup-uniform
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int q = EX ? QN - 1 : a.q, F = a.F, P = a.P, ic = EX ? 1 : a.intercept;
-  const int Qn = ic + q, Qw = q + 1;
+  const int Qn = ic + q;
   unsigned long long* hist = (unsigned long long*)sm;  // a.hist_doubles int64 bins
   double* th = sm + a.hist_doubles;        // kCatPMax: theta of this partition
   double* stdv = th + kCatPMax;            // 2 x kCatQMax: center, 1 / scale
@@ -104,7 +119,7 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
   __shared__ int4 dtab[kCatMaxFactors / 4];  // first dummy parameter of each factor
   int32_t* t_doff = (int32_t*)dtab;
   for (int i = tid; i <= FM; i += NTHR)
-    ftab[i] = i < F ? make_int4(a.nd_rep[i] - 1, a.nlev[i], a.nd_off[i], a.g_off[i])
+    ftab[i] = i < F ? make_int4(a.nd_rep[i] - 1, a.nd_lev[i], a.nd_off[i], a.g_off[i])
                     : make_int4(0, 0, 0, 0);
   for (int i = tid; i <= NPM; i += NTHR) {
     int f = 0, g = i;  // position i = cat_pair(f, g, FM)
@@ -135,16 +150,48 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
   for (int i = 0; i < QN + 2; ++i)
     hsc[i] = (i < 2 + q && i < kCatQMax + 2) ? a.hscale[(int64_t)part * (kCatQMax + 2) + i] : 0.0;
   const double* hs = a.hscale + (int64_t)part * (kCatQMax + 2);  // the epilogue's
-  double hacc[NTRI], gacc[QN], llacc = 0.0;
+  double hacc[NTRI], gacc[NQ], llacc = 0.0;
 #pragma unroll
   for (int i = 0; i < NTRI; ++i) hacc[i] = 0.0;
 #pragma unroll
-  for (int i = 0; i < QN; ++i) gacc[i] = 0.0;
+  for (int i = 0; i < NQ; ++i) gacc[i] = 0.0;
+  const int fold = EX ? __builtin_amdgcn_readfirstlane(a.fold) : -1;
 
+  // Software-pipelined row loop (DLSA_CAT_PF, default): the next row's x,
+  // codes and y are loaded once the current row's triangle, gradient and
+  // fixed-point terms are formed -- its x registers are dead by then -- so the
+  // load latency runs under the current row's ~65 LDS atomics instead of
+  // stalling the top of the next iteration (2 waves per SIMD: one workgroup's
+  // histograms fill the CU's LDS).  Rows past the chunk load the chunk's last
+  // row (a valid address, never used).
+  double xl[QN];
+  int cl[FM];
+  double yl;
+  auto load_row = [&](int rr) {
+    const int64_t rw = row0 + rr;
+    const int64_t rl = (DLSA_CAT_ABLATE & 32) ? row0 + (rr & 1023) % nrows : rw;
+    const double* xr = a.Xn + rl * q;
+    const uint8_t* cr = a.codes + rl * F;
+#pragma unroll
+    for (int i = 0; i < QN; ++i) {
+      const int j = i - ic;
+      xl[i] = (i < Qn && j >= 0) ? xr[j] : 0.0;
+    }
+    // unconditional byte loads (a factor past F re-reads the row's last code;
+    // its uses are masked by f < F): a load under f < F would be sunk into a
+    // branch region of its own, next to its first use.  F = 0 (no factors: the
+    // codes may be a null pointer) skips them all, a uniform branch
+    if (F > 0) {
+#pragma unroll
+      for (int f = 0; f < FM; ++f) cl[f] = (int)cr[f < F ? f : F - 1];
+    } else {
+#pragma unroll
+      for (int f = 0; f < FM; ++f) cl[f] = 0;
+    }
+    yl = a.y[rl];
+  };
+  if (tid < nrows) load_row(tid);
   for (int r = tid; r < nrows; r += NTHR) {
-    const int64_t row = row0 + r;
-    const double* xr = a.Xn + row * q;
-    const uint8_t* cr = a.codes + row * F;
     // parameter-order numeric vector: [1 if intercept] x_0 .. x_{q-1} (standardised)
     double xv[QN];
 #pragma unroll
@@ -155,7 +202,7 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
         if (j < 0) {
           v = 1.0;
         } else {
-          v = xr[j];
+          v = xl[i];
           if constexpr (STD) v = (v - stdv[j]) * stdv[kCatQMax + j];
         }
       }
@@ -163,11 +210,8 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
     }
     int cv[FM];
 #pragma unroll
-    for (int f = 0; f < FM; ++f) cv[f] = f < F ? (int)cr[f] : 0;
-    // y with the row's x and codes, one memory round trip per row (left to the
-    // compiler, its load sinks below the exp and costs a second round trip)
-    double yv = a.y[row];
-    asm volatile("" : "+v"(yv));
+    for (int f = 0; f < FM; ++f) cv[f] = cl[f];
+    const double yv = yl;
 
     double e0 = 0.0, e1 = 0.0;
 #pragma unroll
@@ -204,12 +248,27 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
     llacc += yv * e - (fmax(e, 0.0) + log1p(ea));
 
 #pragma unroll
-    for (int i = 0; i < QN && !(DLSA_CAT_ABLATE & 8); ++i) {
-      gacc[i] = fma(res, xv[i], gacc[i]);
+    for (int i = Q0; i < QN && !(DLSA_CAT_ABLATE & 8); ++i) {
+      const int ii = i - Q0;
+      gacc[ii] = fma(res, xv[i], gacc[ii]);
       const double wxi = w * xv[i];
 #pragma unroll
-      for (int j = 0; j <= i; ++j) hacc[i * (i + 1) / 2 + j] = fma(wxi, xv[j], hacc[i * (i + 1) / 2 + j]);
+      for (int j = Q0; j <= i; ++j)
+        hacc[ii * (ii + 1) / 2 + j - Q0] = fma(wxi, xv[j], hacc[ii * (ii + 1) / 2 + j - Q0]);
     }
+    // the row's fixed-point terms, formed once for all factors: [0] w,
+    // [1] residual, [2 + i - ic] w x_i
+    unsigned long long ut[QN + 2];
+    ut[0] = fx_term(w, hsc[0]);
+    ut[1] = fx_term(res, hsc[1]);
+#pragma unroll
+    for (int i = 0; i < QN; ++i)  // parameter i is numeric column i - ic: scale hsc[2 + i - ic]
+      if (i >= ic) ut[2 + i - ic] = fx_term(w * xv[i], ic ? hsc[i + 1] : hsc[i + 2]);
+#if DLSA_CAT_PF
+    __builtin_amdgcn_sched_barrier(0);
+    load_row(min(r + NTHR, nrows - 1));  // the next row, in flight under the atomics
+    __builtin_amdgcn_sched_barrier(0);
+#endif
 
     // one-hot blocks: fixed-point histograms in LDS
     // The record of factor f + 1 (pair p + 1) is read before factor f's (pair
@@ -221,20 +280,17 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
 #pragma unroll
     for (int f = 0; f < FM; ++f) {
       const int4 tn = ftab[f + 1];
-      if (f < F && cv[f] > 0) {
-        const int slot = (lane & tf.x) * tf.y + cv[f] - 1;
+      if (f < F && (cv[f] > 0 || (EX && f == fold))) {
+        // a baseline row of the fold factor goes to its extra slot (the last)
+        const int slot = (lane & tf.x) * tf.y + (cv[f] > 0 ? cv[f] - 1 : tf.y - 1);
         unsigned long long* h = hist + tf.z + slot * a.nd_stride;
         if constexpr (!(DLSA_CAT_ABLATE & 1)) {
-          lds_add(h, w, hsc[0]);
+          lds_add_u(h, ut[0]);
 #pragma unroll
-          for (int i = 0; i < QN; ++i) {  // numeric columns (register index compile-time)
-            // parameter i is numeric column i - ic: scale hsc[2 + i - ic]
-            // (both candidate indices compile-time: no dynamic register index)
-            const double sc = ic ? hsc[i + 1] : hsc[i + 2];
-            if (i >= ic && i < Qn) lds_add(h + 1 + (i - ic), w * xv[i], sc);
-          }
+          for (int i = 0; i < QN; ++i)  // numeric columns (register index compile-time)
+            if (i >= ic && i < Qn) lds_add_u(h + 1 + (i - ic), ut[2 + i - ic]);
         }
-        if constexpr (!(DLSA_CAT_ABLATE & 4)) lds_add(hist + tf.w + slot, res, hsc[1]);
+        if constexpr (!(DLSA_CAT_ABLATE & 4)) lds_add_u(hist + tf.w + slot, ut[1]);
       }
       tf = tn;
     }
@@ -248,10 +304,13 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
         const int pn = cat_pair(f, g, FM) + 2;
         const int4 tn = ptab[pn <= kCatMaxPairs ? pn : kCatMaxPairs];
         if (!(DLSA_CAT_ABLATE & 2) && g < F && cv[f] > 0 && cv[g] > 0)
-          lds_add(hist + tp.x + ((lane & tp.y) * tp.z + cv[f] - 1) * tp.w + cv[g] - 1, w, hsc[0]);
+          lds_add_u(hist + tp.x + ((lane & tp.y) * tp.z + cv[f] - 1) * tp.w + cv[g] - 1, ut[0]);
         tp = tp1;
         tp1 = tn;
       }
+#if !DLSA_CAT_PF
+    if (r + NTHR < nrows) load_row(r + NTHR);
+#endif
   }
 
   // ---- reduce the register blocks over the workgroup (fixed order) --------
@@ -266,13 +325,13 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
     if (lane == 0) red[wid * NR + i] = v;
   }
 #pragma unroll
-  for (int i = 0; i < QN; ++i) {
+  for (int i = 0; i < NQ; ++i) {
     const double v = wave_red(gacc[i]);
     if (lane == 0) red[wid * NR + NTRI + i] = v;
   }
   {
     const double v = wave_red(llacc);
-    if (lane == 0) red[wid * NR + NTRI + QN] = v;
+    if (lane == 0) red[wid * NR + NTRI + NQ] = v;
   }
   __syncthreads();
   double* fin = red + NW * NR;
@@ -301,10 +360,23 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
   };
   // exact integer sums over the replicas, one rounding back to fp64
   auto nd_sum = [&](int f, int lev, int col) {
-    const int4 r = ftab[f];  // {R - 1, levels, nd offset, g offset}
+    const int4 r = ftab[f];  // {R - 1, level slots, nd offset, g offset}
     long long s = 0;
     for (int rp = 0; rp <= r.x; ++rp) s += hist_at(hist, r.z + (rp * r.y + lev) * a.nd_stride + col);
     return (double)s / (col == 0 ? hsl[0] : hsl[1 + col]);
+  };
+  // EX: the intercept row -- the fold factor's bins over every level slot
+  // (baseline included) and replica, exact in int64, one rounding.  col -1:
+  // the gradient histogram
+  auto fold_sum = [&](int col) {
+    const int4 r = ftab[EX ? fold : 0];  // (called in EX kernels only)
+    long long s = 0;
+    for (int rp = 0; rp <= r.x; ++rp)
+      for (int l = 0; l < r.y; ++l)
+        s += col < 0 ? hist_at(hist, r.w + rp * r.y + l)
+                     : hist_at(hist, r.z + (rp * r.y + l) * a.nd_stride + col);
+    const int si = col < 0 ? 1 : col == 0 ? 0 : 1 + col;  // its grid (hsl layout above)
+    return (double)s / hsl[si];
   };
 
   // ---- epilogue: the partial slab in the dense pass's tile format ---------
@@ -320,7 +392,10 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
     double v = 0.0;
     if (!(DLSA_CAT_ABLATE & 16) && gi < P && gj <= gi) {
       if (gi < Qn) {
-        v = fin[gi * (gi + 1) / 2 + gj];
+        if (EX && gj == 0)
+          v = fold_sum(gi);  // ic = 1: parameter gi >= 1 is bin column gi (w x_{gi - 1})
+        else
+          v = fin[(gi - Q0) * (gi - Q0 + 1) / 2 + gj - Q0];
       } else {
         int li;
         const int fi = factor_of(gi, li);
@@ -347,7 +422,7 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
   for (int e = tid; e < PP; e += NTHR) {
     double v = 0.0;
     if (e < Qn) {
-      v = fin[NTRI + e];
+      v = (EX && e == 0) ? fold_sum(-1) : fin[NTRI + e - Q0];
     } else if (e < P) {
       int l;
       const int f = factor_of(e, l);
@@ -358,7 +433,7 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
     }
     a.slab_g[(int64_t)chunk * PP + e] = v;
   }
-  if (tid == 0) a.slab_ll[chunk] = fin[NTRI + QN];
+  if (tid == 0) a.slab_ll[chunk] = fin[NTRI + NQ];
 }
 
 // Level presence per chunk: counts[chunk, d] = 1 if a row of the chunk
@@ -517,8 +592,8 @@ __global__ __launch_bounds__(256) void cat_mark_kernel(const CatArgs a, const in
 
 template <int QN, int FM, int NTHR, bool STD>
 static hipError_t launch_cat_t(const CatArgs& a, int n_chunks, size_t lds, hipStream_t s) {
-  // the exact-bucket kernel only where it exists (F <= 8)
-  const bool ex = FM == 8 && a.intercept == 1 && a.q + 1 == QN;
+  // the exact-bucket kernel only where it exists (F <= 8) and folds (F >= 1)
+  const bool ex = FM == 8 && cat_exact_bucket(a) && a.fold >= 0;
   auto kern = ex ? cat_pass_kernel<QN, FM, NTHR, STD, FM == 8> : cat_pass_kernel<QN, FM, NTHR, STD, false>;
   {
     hipError_t e = ensure_max_lds((const void*)kern, 160 * 1024 - kCatStaticLds);
@@ -529,13 +604,18 @@ static hipError_t launch_cat_t(const CatArgs& a, int n_chunks, size_t lds, hipSt
 }
 
 static int cat_qn(int Qn) { return Qn <= 4 ? 4 : Qn <= 8 ? 8 : Qn <= 10 ? 10 : Qn <= 12 ? 12 : 16; }
+// the exact-bucket instantiation (EX): intercept fitted, 1 + q equal to its
+// column bucket, 1 <= F <= 8 (the host layout then names a fold factor)
+bool cat_exact_bucket(const CatArgs& a) {
+  return a.intercept == 1 && a.F >= 1 && a.F <= 8 && a.q + 1 == cat_qn(1 + a.q);
+}
 static constexpr int cat_threads_t(int QN, int FM) {
   return (QN <= 4 || (QN <= 10 && FM <= 8)) ? 512 : 256;
 }
 
 size_t cat_lds_bytes(const CatArgs& a) {
   const int QN = cat_qn(a.intercept + a.q);
-  const int NR = QN * (QN + 1) / 2 + QN + 1;
+  const int NR = QN * (QN + 1) / 2 + QN + 1;  // (the EX kernel's NR is smaller)
   const int NW = cat_threads_t(QN, a.F <= 8 ? 8 : 16) / 64;
   return 8 * ((size_t)a.hist_doubles + kCatPMax + 2 * kCatQMax + (size_t)(NW + 1) * NR);
 }

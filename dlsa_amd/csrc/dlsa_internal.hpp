@@ -23,7 +23,11 @@ enum : int32_t {
   PHASE_F64 = 1,
   PHASE_F32X = 2,
   PHASE_DONE = 3,
-  PHASE_LEVEL_DONE = 4
+  PHASE_LEVEL_DONE = 4,
+  // host-set for one launch only: a PHASE_F64 partition whose max |z| record
+  // is stale, routed to the fp64-MFMA exact pass beside an int8 pass of the
+  // fresh ones (capi.hip fused_pass); restored to PHASE_F64 before the solve
+  PHASE_F64_STALE = 5
 };
 constexpr int kRunPhases = 3;
 enum : int32_t { STATUS_RUNNING = -1 };
@@ -275,6 +279,12 @@ struct CatArgs {
   int32_t nd_stride;          // 8-byte words per (replica, level) row of an nd histogram: q + 1
                               // rounded up to odd (the lanes' rows then fall on distinct banks)
   int32_t nlev[kCatMaxFactors];    // dummy columns of factor f (L_f - 1)
+  int32_t nd_lev[kCatMaxFactors];  // level slots per replica of f's nd / gradient histograms:
+                                   // nlev, + 1 for the fold factor (its baseline level)
+  int32_t fold;                    // the exact-bucket kernel's fold factor, else -1: its
+                                   // histograms also take the baseline level, so the
+                                   // intercept row of X^T W X and gradient are the sums of
+                                   // its levels (no register accumulators for them)
   int32_t doff[kCatMaxFactors];    // parameter index of factor f's first dummy
   int32_t nd_off[kCatMaxFactors];  // LDS: [rep][nlev][q + 1] (w, w x_0 ..)
   int32_t nd_rep[kCatMaxFactors];  // replicas (power of two)
@@ -303,6 +313,7 @@ hipError_t launch_partition_scatter(const int32_t* pid, int64_t n, int K, int64_
 // Launchers (defined in the .hip files).
 hipError_t launch_cat_pass(const CatArgs& a, bool standardize, int n_chunks, hipStream_t s);
 size_t cat_lds_bytes(const CatArgs& a);  // dynamic LDS of the pass
+bool cat_exact_bucket(const CatArgs& a);  // the pass's exact-bucket kernel applies (fold factor)
 constexpr int kCatStaticLds =  // its tables: factor and pair records, dummy offsets
     16 * (kCatMaxFactors + 1) + 16 * (kCatMaxPairs + 1) + 4 * kCatMaxFactors;
 hipError_t launch_cat_presence(const CatArgs& a, int n_chunks, int32_t* counts, int32_t* bad,

@@ -596,7 +596,7 @@ __device__ __forceinline__ void oz_producer_r4(const PassArgs& a, char* smem, in
                                                int tid, int nb, int nit, int sbytes,
                                                int xs_bytes, SlotX&& slot_x, const double* bet,
                                                const double* stdv, const int* ex, int chunk,
-                                               Dma&& issue_pair) {
+                                               bool chunk_ovf, Dma&& issue_pair) {
   using namespace ozk;
   static_assert(ND == 5 && DLSA_OZ_MAGICF, "row-quad producers: 5 digits, magic constants");
   constexpr int PMAX = 16 * NT;
@@ -800,7 +800,10 @@ __device__ __forceinline__ void oz_producer_r4(const PassArgs& a, char* smem, in
     double sg = 0.0;
 #pragma unroll
     for (int w = 0; w < NPW; ++w) sg += red[w * (PMAX + 1) + PMAX];
-    a.slab_ll[chunk] = sg;
+    // a digit exponent past EMAX (clamped in ex[]) would publish wrapped
+    // digits: the chunk's NaN log-likelihood fails its partition visibly
+    // (chunk_ovf is wave 0's ballot; tid 0 is in wave 0)
+    a.slab_ll[chunk] = chunk_ovf ? __builtin_nan("") : sg;
   }
 }
 
@@ -1078,7 +1081,7 @@ __global__ __launch_bounds__(64 * (ozk::NPW + ozk::NCW), 1) void irls_oz_kernel(
 
 #if DLSA_OZ_R4
   oz_producer_r4<NT, STD, FAM>(a, smem, wid, lane, tid, nb, nit, sbytes, xs_bytes, slot_x, bet,
-                               stdv, ex, chunk, issue_pair);
+                               stdv, ex, chunk, chunk_ovf, issue_pair);
   return;
 #endif
   // ========================= producer waves ==================================

@@ -83,7 +83,6 @@ __global__ __launch_bounds__(NTHR) void newton_solve_kernel(const SolveArgs a) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   constexpr int T = NT * (NT + 1) / 2;
   constexpr int PP = 16 * NT;
-  constexpr int R = (PP + 63) / 64;  // solve registers per lane (rows lane + 64 r)
   const int k = blockIdx.x;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
@@ -153,6 +152,7 @@ __global__ __launch_bounds__(NTHR) void newton_solve_kernel(const SolveArgs a) {
     double s = 0.0;
     for (int c = cb; c < ce; ++c) s += a.slab_g[(int64_t)c * PP + tid];
     g[tid] = s;
+    z[tid] = s;  // the augmented row of the factorisation: becomes L^-1 g (step 4)
   }
   if (wid == 0) {
     double s = 0.0;
@@ -296,10 +296,14 @@ __global__ __launch_bounds__(NTHR) void newton_solve_kernel(const SolveArgs a) {
       ok = false;
       break;
     }
-    if (c0 + 16 < P) {
-      const int i = c0 + 16 + tid;
-      if (i < P) {
-        double* hr = H + tri(i, c0);
+    // (b) panel rows below the block, and the augmented row z (thread
+    //     nbelow): its block entries become z_b = L_bb^-1 (g_b - sum_c L_bc z_c),
+    //     the forward substitution L z = g folded into the factorisation (the
+    //     serial per-column forward loop of step 5 is gone)
+    const int nbelow = max(0, P - (c0 + 16));
+    if (tid <= nbelow) {
+      {
+        double* hr = tid < nbelow ? H + tri(c0 + 16 + tid, c0) : z + c0;
         double x[16];
 #pragma unroll
         for (int kk = 0; kk < 16; ++kk) x[kk] = hr[kk];
@@ -312,8 +316,18 @@ __global__ __launch_bounds__(NTHR) void newton_solve_kernel(const SolveArgs a) {
 #pragma unroll
         for (int kk = 0; kk < 16; ++kk) hr[kk] = x[kk];
       }
-      __syncthreads();
-      SOLVE_PAN(2)
+    }
+    __syncthreads();
+    SOLVE_PAN(2)
+    if (c0 + 16 < P) {
+      // (c0) the augmented row's trailing update: z_j -= L_jb z_b, j below
+      for (int jj = tid; jj < nbelow; jj += kSolveThreads) {
+        const double* lr = H + tri(c0 + 16 + jj, c0);
+        double acc = 0.0;
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) acc = fma(lr[kk], z[c0 + kk], acc);
+        z[c0 + 16 + jj] -= acc;
+      }
       const int m = NT - b - 1;  // tile rows below the panel
       const int ntile = m * (m + 1) / 2;
       const int fl = lv & 15, q = lv >> 4;
@@ -374,91 +388,46 @@ __global__ __launch_bounds__(NTHR) void newton_solve_kernel(const SolveArgs a) {
   }
 
   SOLVE_MARK(3)
-  // 5. triangular solves L z = g, L^T d = z by wave 0 (no barriers: lane l
-  //    holds z[l + 64 r]).  The pivot's owner lane scales it by 1 / L_jj and
-  //    v_readlane broadcasts it (no LDS round trip on the recurrence); the
-  //    L entries of 4 steps are read ahead, off the dependency chain
-  //    (P = 182: 239k -> see DESIGN.md cycles per solve pair).  Same
-  //    arithmetic, in the same order, as a per-step shuffle.
-  if (wid == 0) {
-    constexpr int U = 4;
-    double zr[R], ir[R];
-    const double* hrow[R];  // row base of lane row i (clamped to P - 1): L[i][j] = hrow[j]
+  // 5. back substitution L^T d = z (L z = g came out of step 4 as the
+  //    augmented row), blocked by the 16-column panels from the last: wave 0
+  //    solves the block's L_bb^T d_b = z_b in registers (lane i = row i, the
+  //    pivot broadcast by v_readlane, 1 / L_kk from invd), then every thread j
+  //    of the columns left of the block takes z_j -= sum_k L[c0 + k][j] d_k.
+  //    Two barriers per 16 columns instead of a serial chain of P steps.
+  for (int b = (P - 1) >> 4; b >= 0; --b) {
+    const int c0 = 16 * b;
+    const int nb = min(16, P - c0);
+    int lv = lane;
+    asm volatile("" : "+v"(lv));
+    if (wid == 0) {
+      const int i = lv & 15;
+      const bool act = lv < nb;
+      // L[c0 + m][c0 + i] for m > i (the block's column i), zero elsewhere
+      double lc[16];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int i = lane + 64 * r;
-      zr[r] = i < P ? g[i] : 0.0;
-      ir[r] = i < P ? invd[i] : 0.0;
-      hrow[r] = H + tri(min(i, P - 1), 0);
-    }
-    for (int j0 = 0; j0 < P; j0 += U) {
-      // lane index re-defined per step group (no hoisted lane masks to spill);
-      // unconditional loads (row base + j stays inside the allocation; the
-      // entries off the strict lower triangle are selected away)
-      int lv = lane;
-      asm volatile("" : "+v"(lv));
-      double hv[U][R];
+      for (int m = 0; m < 16; ++m)
+        lc[m] = *((act && m > i && m < nb) ? H + tri(c0 + m, c0 + i) : red + kRedZero);
+      double zi = act ? z[c0 + i] : 0.0;
+      const double il = act ? invd[c0 + i] : 0.0;
 #pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const int i = lv + 64 * r, j = j0 + u;
-          // off the strict lower triangle: the zero word (an address select,
-          // one v_cndmask instead of two on the loaded value)
-          hv[u][r] = *((j < P && i > j && i < P) ? hrow[r] + j : red + kRedZero);
-        }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int j = j0 + u;
-        if (j < P) {  // wave-uniform
-          double zs = 0.0;
-#pragma unroll
-          for (int r = 0; r < R; ++r)
-            if ((j >> 6) == r) zs = zr[r] * ir[r];
-          const double zj = readlane_f64(zs, j & 63);
-#pragma unroll
-          for (int r = 0; r < R; ++r) {  // branch-free: hv = 0 off the active rows
-            const int i = lv + 64 * r;
-            const double upd = fma(-hv[u][r], zj, zr[r]);
-            zr[r] = i == j ? zj : upd;
-          }
+      for (int kk = 15; kk >= 0; --kk) {
+        if (kk < nb) {  // wave-uniform
+          const double dk = readlane_f64(zi * il, kk);
+          zi = (i == kk) ? dk : fma(-lc[kk], dk, zi);
         }
       }
+      if (act && lv < 16) z[c0 + i] = zi;
     }
-    for (int j0 = P - 1; j0 >= 0; j0 -= U) {
-      int lv = lane;
-      asm volatile("" : "+v"(lv));
-      double hv[U][R];
+    __syncthreads();
+    for (int j = tid; j < c0; j += kSolveThreads) {
+      double acc = 0.0;
 #pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const int i = lv + 64 * r, j = j0 - u;
-          hv[u][r] = *((j >= 0 && i < j) ? H + tri(j, 0) + i : red + kRedZero);
-        }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int j = j0 - u;
-        if (j >= 0) {  // wave-uniform
-          double zs = 0.0;
-#pragma unroll
-          for (int r = 0; r < R; ++r)
-            if ((j >> 6) == r) zs = zr[r] * ir[r];
-          const double zj = readlane_f64(zs, j & 63);
-#pragma unroll
-          for (int r = 0; r < R; ++r) {
-            const int i = lv + 64 * r;
-            const double upd = fma(-hv[u][r], zj, zr[r]);
-            zr[r] = i == j ? zj : upd;
-          }
-        }
-      }
+      for (int k2 = 0; k2 < 16; ++k2)
+        if (k2 < nb) acc = fma(H[tri(c0 + k2, j)], z[c0 + k2], acc);
+      z[j] -= acc;
     }
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-      if (lane + 64 * r < P) z[lane + 64 * r] = zr[r];
+    __syncthreads();
   }
-  __syncthreads();
 
   SOLVE_MARK(4)
 #if DLSA_SOLVE_PROFILE

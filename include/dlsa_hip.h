@@ -161,6 +161,10 @@ typedef struct dlsa_fit_stats {
                                the size without them but smaller than
                                dlsa_logistic_workspace_bytes, a failed
                                allocation, or dlsa_fit_options.oz_max_bytes) */
+  int32_t oz_stale_partitions; /* P <= 112, mixed mode: partition passes of an
+                               exact pass that ran on the fp64 MFMA beside the
+                               int8 launch of the others, for lack of a fresh
+                               max |sqrt(w) x| record */
 } dlsa_fit_stats;
 
 /* Default options (mixed Hessian, automatic chunking, no timing). */

@@ -18,6 +18,8 @@ for v in "$@"; do
     cat16) D=DLSA_CAT_ABLATE=16 ;;
     cat8) D=DLSA_CAT_ABLATE=8 ;;
     catpf0) D=DLSA_CAT_PF=0 ;;
+    catnd256) D=DLSA_CAT_ND_CAP=256 ;;
+    catnd512) D=DLSA_CAT_ND_CAP=512 ;;
     catpf1) D=DLSA_CAT_PF=1 ;;
     cat32) D="DLSA_CAT_PF=0 -DDLSA_CAT_ABLATE=32" ;;
     catpf32) D=DLSA_CAT_ABLATE=32 ;;
@@ -68,6 +70,7 @@ for v in "$@"; do
   case $v in
     oz*|ozs*) ONLY='["irls_oz.hip", "irls_oz_g2.hip"]' ;;
     solve*) ONLY='["newton_solve.hip"]' ;;
+    catnd*) ONLY='["capi.hip"]' ;;
     cat*) ONLY='["cat_pass.hip"]' ;;
     olswave|olsks2|olsks8|olsks12|olsks16) ONLY='["ols_stream.hip"]' ;;
     olsks2k) ONLY='["ols_stream.hip", "capi.hip"]' ;;
