@@ -145,6 +145,79 @@ static int32_t* pinned_staging(size_t n_i32) {
   return buf;
 }
 
+// Pinned host staging of the chunk tables a fit uploads at its start and at
+// every warm-start level change.  From pageable vectors hipMemcpyAsync copies
+// through the runtime's own staging and returns when the copy is done: the
+// first such copy of a process took 16.7 ms at config 2's level change
+// (profiles/r06d_first_fit_trace.txt), with the GPU idle behind it.  From
+// here the copies are asynchronous.  Thread-local, grown on demand at a fit's
+// start (reserve: every plan of the fit), never shrunk; an event after the
+// last staged copy guards the reuse by the next fit (a fit that fails early
+// returns without its final synchronisation).
+struct PinnedArena {
+  char* buf = nullptr;
+  size_t cap = 0, used = 0;
+  hipEvent_t done = nullptr;
+  bool pending = false;
+};
+static PinnedArena& pinned_arena() {
+  thread_local PinnedArena a;
+  return a;
+}
+static hipError_t pinned_arena_reserve(size_t bytes) {
+  PinnedArena& a = pinned_arena();
+  if (a.pending) {
+    hipError_t e = hipEventSynchronize(a.done);
+    if (e != hipSuccess) return e;
+    a.pending = false;
+  }
+  a.used = 0;
+  if (!a.done) {
+    hipError_t e = hipEventCreateWithFlags(&a.done, hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+  }
+  if (a.cap >= bytes) return hipSuccess;
+  char* nb = nullptr;
+  hipError_t e = hipHostMalloc((void**)&nb, bytes, hipHostMallocDefault);
+  if (e != hipSuccess) return e;
+  if (a.buf) (void)hipHostFree(a.buf);
+  a.buf = nb;
+  a.cap = bytes;
+  return hipSuccess;
+}
+// bytes one call of staged_upload takes from the arena
+static size_t staged_bytes(size_t bytes) { return (size_t)align_up((int64_t)bytes, 64); }
+// H2D copy of host data through the arena (pageable copy if it is full)
+static hipError_t staged_upload(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  if (bytes == 0) return hipSuccess;
+  PinnedArena& a = pinned_arena();
+  if (!a.buf || a.used + staged_bytes(bytes) > a.cap)
+    return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s);
+  char* p = a.buf + a.used;
+  a.used += staged_bytes(bytes);
+  memcpy(p, src, bytes);
+  hipError_t e = hipMemcpyAsync(dst, p, bytes, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipEventRecord(a.done, s);
+  if (e == hipSuccess) a.pending = true;
+  return e;
+}
+// arena bytes of one plan's chunk tables (row0, rows, part, partition chunk begins)
+static size_t plan_staged_bytes(const Plan& q, int K) {
+  return staged_bytes(8 * (size_t)q.n_chunks) + 2 * staged_bytes(4 * (size_t)q.n_chunks) +
+         staged_bytes(4 * ((size_t)K + 1));
+}
+static hipError_t upload_plan_tables(const Plan& q, int K, void* d_row0, void* d_rows,
+                                     void* d_part, void* d_pcb, hipStream_t s) {
+  hipError_t e = hipSuccess;
+  if (q.n_chunks > 0) {
+    e = staged_upload(d_row0, q.chunk_row0.data(), 8LL * q.n_chunks, s);
+    if (e == hipSuccess) e = staged_upload(d_rows, q.chunk_rows.data(), 4LL * q.n_chunks, s);
+    if (e == hipSuccess) e = staged_upload(d_part, q.chunk_part.data(), 4LL * q.n_chunks, s);
+  }
+  if (e == hipSuccess) e = staged_upload(d_pcb, q.part_chunk_begin.data(), 4LL * (K + 1), s);
+  return e;
+}
+
 // fewest rows of a warm-start level per parameter (DLSA_LEVEL_ROWS_PER_P
 // overrides in knob builds, schedule sweeps)
 static int64_t level_rows_per_param() {
@@ -638,23 +711,14 @@ static int fit_wide(int family, const double* X, const double* y, const int64_t*
 
   auto upload_plan = [&](const Plan& q, int64_t o_row0, int64_t o_rows, int64_t o_part,
                          int32_t* d_cb) -> hipError_t {
-    hipError_t e = hipSuccess;
-    if (q.n_chunks > 0) {
-      e = hipMemcpyAsync(at(o_row0), q.chunk_row0.data(), 8LL * q.n_chunks,
-                         hipMemcpyHostToDevice, stream);
-      if (e == hipSuccess)
-        e = hipMemcpyAsync(at(o_rows), q.chunk_rows.data(), 4LL * q.n_chunks,
-                           hipMemcpyHostToDevice, stream);
-      if (e == hipSuccess)
-        e = hipMemcpyAsync(at(o_part), q.chunk_part.data(), 4LL * q.n_chunks,
-                           hipMemcpyHostToDevice, stream);
-    }
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(d_cb, q.part_chunk_begin.data(), 4LL * (K + 1), hipMemcpyHostToDevice,
-                         stream);
-    return e;
+    return upload_plan_tables(q, K, at(o_row0), at(o_rows), at(o_part), d_cb, stream);
   };
-  DLSA_HIP_TRY(hipMemcpyAsync(d_offsets, offsets, 8LL * (K + 1), hipMemcpyHostToDevice, stream));
+  {
+    size_t need = staged_bytes(8 * ((size_t)K + 1));
+    for (const WidePlans& q : plans) need += plan_staged_bytes(q.rows, K) + plan_staged_bytes(q.gram, K);
+    DLSA_HIP_TRY(pinned_arena_reserve(need));
+  }
+  DLSA_HIP_TRY(staged_upload(d_offsets, offsets, 8LL * (K + 1), stream));
 
   // MIXED / MIXED_F32: bf16-MFMA Gram passes until the step is below
   // switch_tol, then fp64 Gram passes (the fused path's phase machine)
@@ -910,23 +974,9 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
   int32_t* d_cnt = (int32_t*)at(L.off_counters);
 
   auto upload = [&](const Plan& q) -> hipError_t {
-    hipError_t e = hipSuccess;
-    if (q.n_chunks > 0) {
-      e = hipMemcpyAsync(d_row0, q.chunk_row0.data(), 8LL * q.n_chunks, hipMemcpyHostToDevice,
-                         stream);
-      if (e == hipSuccess)
-        e = hipMemcpyAsync(d_rows, q.chunk_rows.data(), 4LL * q.n_chunks,
-                           hipMemcpyHostToDevice, stream);
-      if (e == hipSuccess)
-        e = hipMemcpyAsync(d_part, q.chunk_part.data(), 4LL * q.n_chunks,
-                           hipMemcpyHostToDevice, stream);
-    }
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(d_pcb, q.part_chunk_begin.data(), 4LL * (K + 1), hipMemcpyHostToDevice,
-                         stream);
-    return e;
+    return upload_plan_tables(q, K, d_row0, d_rows, d_part, d_pcb, stream);
   };
-  DLSA_HIP_TRY(hipMemcpyAsync(d_offsets, offsets, 8LL * (K + 1), hipMemcpyHostToDevice, stream));
+  // (the arena is reserved below, once the warm-start level plans are known)
 
   // warm-start levels: Newton on row prefixes (1/16, 1/4) before all rows
   std::vector<Plan> plans;
@@ -941,6 +991,12 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
     }
   }
   plans.push_back(pl);
+  {
+    size_t need = staged_bytes(8 * ((size_t)K + 1));
+    for (const Plan& q : plans) need += plan_staged_bytes(q, K);
+    DLSA_HIP_TRY(pinned_arena_reserve(need));
+  }
+  DLSA_HIP_TRY(staged_upload(d_offsets, offsets, 8LL * (K + 1), stream));
 
   if (family == FAMILY_GAUSSIAN) max_iter = 1;  // closed form: one exact fp64 pass
   const int start_phase =
@@ -1208,7 +1264,7 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
 // level slots x replicas per factor of the numeric x dummy histograms before
 // the LDS budget shrinks them (A/B builds: DLSA_CAT_ND_CAP)
 #ifndef DLSA_CAT_ND_CAP
-#define DLSA_CAT_ND_CAP 128
+#define DLSA_CAT_ND_CAP 256
 #endif
 // LDS layout of the histograms: replicas so that a frequent level does not
 // serialise the lanes of a wave on one address (nd: <= 128 slots per factor,
@@ -1411,23 +1467,17 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
   double* d_hs = (double*)at(off_hs);
 
   auto upload = [&](const Plan& qn) -> hipError_t {
-    hipError_t e = hipSuccess;
-    if (qn.n_chunks > 0) {
-      e = hipMemcpyAsync(d_row0, qn.chunk_row0.data(), 8LL * qn.n_chunks, hipMemcpyHostToDevice,
-                         stream);
-      if (e == hipSuccess)
-        e = hipMemcpyAsync(d_rows, qn.chunk_rows.data(), 4LL * qn.n_chunks,
-                           hipMemcpyHostToDevice, stream);
-      if (e == hipSuccess)
-        e = hipMemcpyAsync(d_part, qn.chunk_part.data(), 4LL * qn.n_chunks,
-                           hipMemcpyHostToDevice, stream);
-    }
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(d_pcb, qn.part_chunk_begin.data(), 4LL * (K + 1),
-                         hipMemcpyHostToDevice, stream);
-    return e;
+    return upload_plan_tables(qn, K, d_row0, d_rows, d_part, d_pcb, stream);
   };
-  DLSA_HIP_TRY(hipMemcpyAsync(d_offsets, offsets, 8LL * (K + 1), hipMemcpyHostToDevice, stream));
+  {
+    // every level is uploaded once, the final plan twice (presence pass, then
+    // again after the warm-start levels)
+    size_t need = staged_bytes(8 * ((size_t)K + 1)) + plan_staged_bytes(pl, K) +
+                  staged_bytes(8 * ((size_t)kCatQMax + 2) * K);  // + the grids
+    for (const Plan& qn : plans) need += plan_staged_bytes(qn, K);
+    DLSA_HIP_TRY(pinned_arena_reserve(need));
+  }
+  DLSA_HIP_TRY(staged_upload(d_offsets, offsets, 8LL * (K + 1), stream));
   DLSA_HIP_TRY(launch_fit_init(d_offsets, K, P, PHASE_F64, theta, d_phase, d_bt, iters, status,
                                d_llprev, sig_inv, loglik, stream));
 
@@ -1470,7 +1520,7 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
   }
   DLSA_HIP_TRY(hipMemcpyAsync(h_phase, d_phase, 4LL * K, hipMemcpyDeviceToHost, stream));
   DLSA_HIP_TRY(hipStreamSynchronize(stream));
-  std::vector<double> h_hs;  // the grids (alive until the fit's next stream sync)
+  std::vector<double> h_hs;  // the grids (staged into the pinned arena on upload)
   {
     // fixed-point grids: 2^E with |term| * 2^E * max(rows of a chunk, 1024) <= 2^60,
     // so a bin's sum stays in int64 and every term below 2^50 (the kernel's
@@ -1504,8 +1554,7 @@ static int fit_categorical(const double* Xn, const uint8_t* codes, const double*
         o[2 + j] = grid(0.25 * m);
       }
     }
-    DLSA_HIP_TRY(hipMemcpyAsync(d_hs, h_hs.data(), 8LL * (kCatQMax + 2) * K,
-                                hipMemcpyHostToDevice, stream));
+    DLSA_HIP_TRY(staged_upload(d_hs, h_hs.data(), 8LL * (kCatQMax + 2) * K, stream));
     ca.hscale = d_hs;
   }
   for (int k = 0; k < K; ++k)

@@ -13,6 +13,7 @@
 #   bench:<name>:<bench args>   python bench.py <args> -> <name>.json + a summary line
 #   prof:<name>:<bench args>    rocprofv3 --kernel-trace --stats of bench.py -> prof_<name>/
 #                               and <name>_kernel_stats.csv (tools/rocpd_stats.py)
+#   profpy:<name>:<script args> rocprofv3 --kernel-trace --stats of a Python script -> profpy_<name>/
 #   trace:<name>:<bench args>   rocprofv3 --runtime-trace --kernel-trace (csv; no counters)
 #                               -> trace_<name>/ (host API calls beside the kernels)
 #   pmc:<name>:<counters>:<bench args>
@@ -67,6 +68,11 @@ for step in "$@"; do
       db=$(find "$OUT/prof_$name" -name run_results.db | head -1)
       [ -n "$db" ] && python3 tools/rocpd_stats.py "$db" > "$OUT/${name}_kernel_stats.csv" && \
         head -8 "$OUT/${name}_kernel_stats.csv" ;;
+    profpy)
+      name=${rest%%:*}; args=${rest#*:}
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/profpy_$name" -o run -- \
+        python3 $args > "$OUT/profpy_$name.txt" 2> "$OUT/profpy_$name.err" || exit $?
+      tail -12 "$OUT/profpy_$name.txt" ;;
     trace)
       name=${rest%%:*}; args=${rest#*:}
       timeout -k 10 600 rocprofv3 --runtime-trace --kernel-trace --output-format csv -d "$OUT/trace_$name" \
