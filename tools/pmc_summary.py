@@ -59,7 +59,8 @@ assert fetch and write, (len(fetch), len(write))
 per_launch = (2 * sum(fetch) / len(fetch) + sum(write) / len(write)) * 1024
 tf = os.path.join(root, "profiles", "pmc_traffic.json")
 d = json.load(open(tf)) if os.path.exists(tf) else {}
-d[f"config{config}"] = {
+rec_key = os.environ.get("PMC_RECORD_KEY", f"config{config}")
+d[rec_key] = {
     "n": int(n), "p": int(p), "kernel_key": key, "kernel": full[0]["kernel"],
     "full_pass_launches": len(fetch),
     "hbm_bytes_per_full_launch": per_launch,
@@ -68,8 +69,8 @@ d[f"config{config}"] = {
     "write_size_kb_per_launch": sum(write) / len(write),
     "correction": "2 x FETCH_SIZE (gfx950 half-count) + WRITE_SIZE, KB x 1024; full-data "
                   "dispatches only (largest grid, >= 0.7 x the longest)",
-    "source": f"profiles/{prefix}_pmc.csv (tools/pmc.sh, rocprofv3 --pmc, one counter group "
-              "per run)",
+    "source": f"profiles/{prefix}_pmc.csv (rocprofv3 --pmc, one counter group per run: "
+              "tools/closing_run.sh / tools/pmc.sh)",
 }
 json.dump(d, open(tf, "w"), indent=1)
-print(json.dumps(d[f"config{config}"], indent=1))
+print(json.dumps(d[rec_key], indent=1))
