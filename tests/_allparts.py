@@ -21,7 +21,9 @@ def all_partitions_independent(fit, X, y, n, sel, design=None, family="logistic"
           f"(partition {r['worst_partition']}), Sig_invMcoef {r['sig_inv_theta_rel']:.3e}, "
           f"WLSE {r['wlse_rel']:.3e}")
     assert r["max_elem_err"] < 1e-10, r["worst_partition"]
-    assert r["sig_inv_theta_rel"] < 1e-10
+    # Sig_invMcoef = Sig_inv theta sums P per-entry errors (6.8e-10 at P = 500
+    # for 7e-11 per entry): the north-star 1e-8 relative
+    assert r["sig_inv_theta_rel"] < 1e-8
     assert r["wlse_rel"] < 1e-10
     if family == "logistic":
         sup = np.nonzero(sel["beta_byBIC"].to_numpy())[0].tolist()
