@@ -126,7 +126,6 @@ static int iter_budget(bool final_level, int it, int max_iter) {
   if (final_level) return std::max(1, max_iter - it);
   return std::min(kLevelIters, (max_iter - it) / 2);
 }
-// a level stops once its max relative step is below this; DLSA_LEVEL_TOL overrides
 // Pinned host staging of the per-iteration readbacks (running counters +
 // phases), grown on demand and kept for the thread's lifetime: a
 // hipHostMalloc / hipHostFree pair per fit costs a pinning call (and the free
@@ -225,6 +224,7 @@ static int64_t level_rows_per_param() {
   return 64;
 }
 
+// a level stops once its max relative step is below this; DLSA_LEVEL_TOL overrides
 static double warm_level_tol(bool fused) {
   if (const char* e = env_knob("DLSA_LEVEL_TOL")) return atof(e);
   return fused ? 0.2 : 0.1;
