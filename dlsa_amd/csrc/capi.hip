@@ -98,9 +98,10 @@ static int64_t rows_used(int64_t nk, double frac, int64_t min_rows) {
 // profiles/r01m_level_sweep.jsonl, 6-step means): one 1/16 level at a
 // 0.2-relative step 101 ms per fit vs 110 ms for 1/16, 1/4 at 0.1 (6 bf16 +
 // 1 fp64 launches instead of 9 + 1: the 1/4 level's passes cost more than
-// the one full pass they save).  Wide path (config 5): 1/16, 1/4 at 0.1
-// kept -- the alternatives were within noise or triggered a second fp64
-// Gram pass (36 ms).
+// the one full pass they save).  Wide path: 1/16, 1/4 at 0.1, with a level
+// dropped when the next has under twice its rows (wide_level_plans; config 5
+// runs 1/4 alone) -- other schedules were within noise, slower (1/4 at a
+// 0.15 tolerance: 56.4 ms fit, r06h) or triggered a second fp64 Gram pass.
 static std::vector<double> warm_level_fracs(bool fused) {
   std::vector<double> f = fused ? std::vector<double>{1.0 / 16.0}
                                 : std::vector<double>{1.0 / 16.0, 1.0 / 4.0};
@@ -429,19 +430,29 @@ static WideLayout make_wide_layout(const std::vector<WidePlans>& plans, int K, i
 
 // The wide path's plans: the warm-start levels (logistic, warm_start) then
 // all rows.  A level that would stream more than half of the rows is
-// skipped (it would cost more than the full passes it saves).
+// skipped (it would cost more than the full passes it saves).  A level
+// whose row count is less than twice the previous level's replaces it: the
+// min_rows floor can lift a small fraction to nearly the next one (config 5:
+// 1/16 of n_k = 156250 is raised to 64 x 500 = 32000 rows, the 1/4 level has
+// 39063), and two levels that close cost a level's iterations twice for the
+// same start.  Config 5, one box, 4 A/B pairs (profiles/r06h_level_ab.txt):
+// 1/16 + 1/4 10 iterations, fit 54.1-54.2 ms; 1/4 alone 9, 52.7-52.8 ms.
 static std::vector<WidePlans> wide_level_plans(const int64_t* offsets, int K, int p, int intercept,
                                                int rows_per_chunk, bool levels) {
   std::vector<WidePlans> plans;
   const int P = p + (intercept ? 1 : 0);
   if (levels) {
     const int64_t min_rows = std::max<int64_t>(2048, level_rows_per_param() * P);
+    int64_t prev_rows = 0;
     for (double frac : warm_level_fracs(false)) {
       WidePlans q;
       make_wide_plans(offsets, K, p, intercept, rows_per_chunk, q, frac, min_rows);
       int64_t rows = 0;
       for (int c = 0; c < q.rows.n_chunks; ++c) rows += q.rows.chunk_rows[c];
-      if (rows <= offsets[K] / 2 && q.rows.n_chunks > 0) plans.push_back(std::move(q));
+      if (rows > offsets[K] / 2 || q.rows.n_chunks == 0) continue;
+      if (!plans.empty() && rows < 2 * prev_rows) plans.pop_back();
+      plans.push_back(std::move(q));
+      prev_rows = rows;
     }
   }
   WidePlans fin;
