@@ -39,6 +39,11 @@
 #ifndef DLSA_WN_LOOKAHEAD
 #define DLSA_WN_LOOKAHEAD 1
 #endif
+// wide Newton: the trailing update of the approximate iterations on the f32
+// MFMA (1) or on the fp64 MFMA like the exact ones (0, A/B)
+#ifndef DLSA_WN_F32
+#define DLSA_WN_F32 1
+#endif
 // rows per wave and step of the wide row pass (A/B builds)
 #ifndef DLSA_WIDE_ROW_U
 #define DLSA_WIDE_ROW_U 4
@@ -1121,7 +1126,15 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
   // A22 -= L21 L21^T on lower 16x16 tiles: the two tile columns of the next
   // panel (cols01) or the rest; UT tiles per wave at a time (their C reads
   // issued together: one L2 / MALL latency for UT read-modify-writes); tiles
-  // past the end recompute the last tile and skip the store
+  // past the end recompute the last tile and skip the store.  On the
+  // approximate iterations (the Hessian is the bf16 pass's, ~2^-8 per value)
+  // the products run on the f32 MFMA (32 cycles per 16x16x4 against ~64 for
+  // fp64; C stays fp64): the trailing update is the MFMA-bound phase.  The
+  // two forms' C/D maps differ: lane (kq, fl), register r holds row kq + 4 r
+  // (fp64) or 4 kq + r (f32) of column fl, so C is read and written in the
+  // map of the form in use.
+  const bool lowp = phase == PHASE_F32 && DLSA_WN_F32;
+  const int crow = lowp ? 4 * kq : kq, cstep = lowp ? 1 : 4;
   auto trail = [&](int jb, int m, bool cols01, int w0, int nw) {
     const int ntiles = cols01 ? 2 * m - 1 : (m - 2) * (m - 1) / 2;
     constexpr int UT = 4;
@@ -1139,27 +1152,55 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
           ti[u] += 2;
           tj[u] += 2;
         }
-        const double* cp = H + (int64_t)(jb + CB + 16 * ti[u] + kq) * PP + jb + CB + 16 * tj[u] + fl;
+        const double* cp = H + (int64_t)(jb + CB + 16 * ti[u] + crow) * PP + jb + CB + 16 * tj[u] + fl;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) c[u][r] = cp[4 * r * PP];
+        for (int r = 0; r < 4; ++r) c[u][r] = cp[r * cstep * PP];
       }
 #pragma unroll
       for (int u = 0; u < UT; ++u) {
         d4w acc = d4w{0, 0, 0, 0};
+        if (lowp) {
+          f4w a32 = f4w{0, 0, 0, 0};
 #pragma unroll
-        for (int s = 0; s < CB / 4; ++s) {
-          const double av = Lp[(16 * ti[u] + fl) * LDP + 4 * s + kq];
-          const double bv = Lp[(16 * tj[u] + fl) * LDP + 4 * s + kq];
-          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+          for (int s = 0; s < CB / 4; ++s) {
+            const float av = (float)Lp[(16 * ti[u] + fl) * LDP + 4 * s + kq];
+            const float bv = (float)Lp[(16 * tj[u] + fl) * LDP + 4 * s + kq];
+            a32 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, a32, 0, 0, 0);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[r] = (double)a32[r];
+        } else {
+#pragma unroll
+          for (int s = 0; s < CB / 4; ++s) {
+            const double av = Lp[(16 * ti[u] + fl) * LDP + 4 * s + kq];
+            const double bv = Lp[(16 * tj[u] + fl) * LDP + 4 * s + kq];
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+          }
         }
         if (t0 + nw * u < ntiles) {
-          double* cp = H + (int64_t)(jb + CB + 16 * ti[u] + kq) * PP + jb + CB + 16 * tj[u] + fl;
+          double* cp = H + (int64_t)(jb + CB + 16 * ti[u] + crow) * PP + jb + CB + 16 * tj[u] + fl;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) cp[4 * r * PP] = c[u][r] - acc[r];
+          for (int r = 0; r < 4; ++r) cp[r * cstep * PP] = c[u][r] - acc[r];
         }
       }
     }
   };
+  // the forward solve L z = g rides on the factorization: z_b of block b is
+  // solved by one wave against the diagonal block while the panel below is
+  // solved, and every later row takes the block's terms (z_J -= L_Jb z_b)
+  // right after the panel, so no P-long substitution follows the factor
+  auto zsolve = [&](int jb) {
+    const int i = lane & 31;
+    double zi = z[jb + i];
+#pragma unroll
+    for (int c = 0; c < CB; ++c) {
+      if (i == c) zi *= L11[c * LDP + CB];
+      const double zc = bcast_f64(zi, c);
+      if (i > c) zi = fma(-L11[c * LDP + i], zc, zi);
+    }
+    if (lane < 32) z[jb + i] = zi;
+  };
+  for (int f = tid; f < PP; f += 1024) z[f] = g[f];
   if (wv == 0) factor_diag(0);
   __syncthreads();
   {
@@ -1172,9 +1213,16 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
       WN_STAMP(ta);
       panel_copy(jb, PP - jb - CB, true);
       __syncthreads();
+      if (wv == 15) zsolve(jb);  // rows past 480 do not exist: wave 15 has no panel row
       trsm(PP - jb - CB);
       __syncthreads();
       WN_STAMP(tb);
+      if (tid < PP - jb - CB) {
+        double s = z[jb + CB + tid];
+#pragma unroll
+        for (int c = 0; c < CB; ++c) s = fma(-Lp[tid * LDP + c], z[jb + c], s);
+        z[jb + CB + tid] = s;
+      }
       trail(jb, m, true, wv, 16);
       panel_copy(jb, PP - jb - CB, false);  // L21 to H for the solves
       __syncthreads();
@@ -1216,54 +1264,18 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
     return;
   }
 
-  // 5a. forward solve L z = g, 32-row blocks: the diagonal block by one wave
-  // (lane i = row i, reciprocal pivots off the chain), then the rows below take
-  // the block's terms (their L entries loaded before the block is final)
+  // 5a. the last diagonal block's share of the forward solve
   WN_STAMP(t_s0);
-  for (int f = tid; f < PP; f += 1024) z[f] = g[f];
+  if (wv == 0) zsolve(PP - CB);
   __syncthreads();
-  for (int jb = 0; jb < PP; jb += CB) {
-    const int rest = PP - jb - CB;
-    const int rr = tid - 64;  // waves 1..: the rows below, loaded before the block is final
-    const int ib = jb + CB + rr;
-    double hv[CB];
-    if (wv >= 1 && (wv - 1) * 64 < rest) {
-      const double* hb = H + (int64_t)min(ib, PP - 1) * PP + jb;
-#pragma unroll
-      for (int c = 0; c < CB; ++c) hv[c] = hb[c];
-    }
-    if (wv == 0) {
-      const int i = lane & 31;
-      const double* hr = H + (int64_t)(jb + i) * PP + jb;
-      double lrow[CB];
-#pragma unroll
-      for (int c = 0; c < CB; ++c) lrow[c] = hr[c];  // upper part: zeros (factor_diag)
-      const double ri = 1.0 / hr[i];
-      double zi = z[jb + i];
-#pragma unroll
-      for (int c = 0; c < CB; ++c) {
-        if (i == c) zi *= ri;
-        const double zc = bcast_f64(zi, c);
-        if (i > c) zi = fma(-lrow[c], zc, zi);
-      }
-      z[jb + i] = zi;
-    }
-    __syncthreads();
-    if (wv >= 1 && rr < rest) {
-      double s = z[ib];
-#pragma unroll
-      for (int c = 0; c < CB; ++c) s = fma(-hv[c], z[jb + c], s);
-      z[ib] = s;
-    }
-    __syncthreads();
-  }
   WN_STAMP(t_s1);
   // 5b. backward solve L^T d = z (d overwrites z): u_c = sum_{i >= jb + CB}
   // L[i][jb + c] d_i in fixed order (4 rows in flight per thread), then
   // L11^T d_b = z_b - u by one wave (lane c = unknown c)
   for (int jb = PP - CB; jb >= 0; jb -= CB) {
+    const int c = tid & 31;
     {
-      const int c = tid & 31, grp = tid >> 5;
+      const int grp = tid >> 5;
       double s = 0.0;
       int i = jb + CB + grp;
       for (; i + 96 < PP; i += 128) {
@@ -1279,7 +1291,6 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
     }
     __syncthreads();
     if (wv == 0) {
-      const int c = lane & 31;
       double lcol[CB];  // column c of L11: L[r][c] (zero above the diagonal)
 #pragma unroll
       for (int r = 0; r < CB; ++r) lcol[r] = H[(int64_t)(jb + r) * PP + jb + c];

@@ -53,6 +53,7 @@ for v in "$@"; do
     cmabl) D=DLSA_CM_ABLATE=1 ;;
     olswave) D=DLSA_OLS_STREAM=0 ;;
     wnold) D=DLSA_WN_LOOKAHEAD=0 ;;
+    wnf64) D=DLSA_WN_F32=0 ;;
     olsks2) D=DLSA_OLS_KS=2 ;;
     olsks2k) D="DLSA_OLS_KS=2 -DDLSA_ENV_KNOBS=1" ;;
     olsks8) D=DLSA_OLS_KS=8 ;;
