@@ -81,7 +81,18 @@ namespace {
 
 constexpr int GT = kWideTile;  // gram output tile edge (128)
 constexpr int CB = 32;         // Cholesky panel width
-constexpr int LDP = CB + 1;    // padded LDS row stride of a panel (doubles)
+// padded LDS row stride of a panel (doubles).  CB + 2: the MFMA operand reads
+// Lp[(16 t + fl) LDP + 4 s + kq] of a 32-lane group (fl < 16, kq < 2) then fall
+// on banks 4 fl + 2 kq (+1), all 64 distinct; CB + 1 put (fl, kq = 1) and
+// (fl + 1, kq = 0) on one bank pair (2-way).  The row-per-thread reads of the
+// panel solve take the 2-way instead (16x fewer instructions).
+#ifndef DLSA_WN_LDP
+#define DLSA_WN_LDP (CB + 2)
+#endif
+constexpr int LDP = DLSA_WN_LDP;
+static_assert(LDP > CB, "the padding slot CB holds the reciprocal pivots");
+static_assert((CB * LDP + DLSA_MAX_P * LDP + 2 * DLSA_MAX_P + 64) * 8 <= 160 * 1024,
+              "wide_newton_kernel LDS at PP = DLSA_MAX_P");
 
 __device__ __forceinline__ double wave_sum64(double v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -1137,7 +1148,7 @@ __global__ __launch_bounds__(1024) void wide_newton_kernel(const SolveArgs a, co
   const int crow = lowp ? 4 * kq : kq, cstep = lowp ? 1 : 4;
   auto trail = [&](int jb, int m, bool cols01, int w0, int nw) {
     const int ntiles = cols01 ? 2 * m - 1 : (m - 2) * (m - 1) / 2;
-    constexpr int UT = 4;
+    constexpr int UT = 4;  // 6 or 8 spill (25 / 57 VGPRs)
     for (int t0 = w0; t0 < ntiles; t0 += nw * UT) {
       int ti[UT], tj[UT];
       d4w c[UT];

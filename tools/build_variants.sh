@@ -54,6 +54,8 @@ for v in "$@"; do
     olswave) D=DLSA_OLS_STREAM=0 ;;
     wnold) D=DLSA_WN_LOOKAHEAD=0 ;;
     wnf64) D=DLSA_WN_F32=0 ;;
+    wnldp33) D=DLSA_WN_LDP=33 ;;
+    wnldp33prof) D="DLSA_WN_LDP=33 -DDLSA_WN_PROF=1" ;;
     olsks2) D=DLSA_OLS_KS=2 ;;
     olsks2k) D="DLSA_OLS_KS=2 -DDLSA_ENV_KNOBS=1" ;;
     olsks8) D=DLSA_OLS_KS=8 ;;
