@@ -53,6 +53,14 @@
 #ifndef DLSA_CAT_PF
 #define DLSA_CAT_PF 1
 #endif
+// Histogram slot order: replica outermost (0: slot = replica * levels + level)
+// or innermost (1, A/B: slot = level * R + replica).  Innermost was meant to put
+// the 16 lanes of an 8-byte LDS atomic group on 16 different bank pairs for
+// the R = 16 factors; it measured slower: 5.71-5.72 vs 5.43-5.47 ms per full
+// config-3 pass, alternated on one box (profiles/r06p_cat_slot_order_ab.txt)
+#ifndef DLSA_CAT_RINNER
+#define DLSA_CAT_RINNER 0
+#endif
 
 namespace dlsa {
 
@@ -72,6 +80,12 @@ __device__ __forceinline__ void lds_add_u(unsigned long long* p, unsigned long l
 }
 __device__ __forceinline__ long long hist_at(const unsigned long long* h, int i) {
   return (long long)h[i];
+}
+
+// histogram slot of level slot lev, replica rp of a factor record
+// {R - 1, level slots, ...}
+__device__ __forceinline__ int cat_slot(const int4 r, int lev, int rp) {
+  return DLSA_CAT_RINNER ? lev * (r.x + 1) + rp : rp * r.y + lev;
 }
 
 // pair index of factors f < g among F
@@ -282,7 +296,7 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
       const int4 tn = ftab[f + 1];
       if (f < F && (cv[f] > 0 || (EX && f == fold))) {
         // a baseline row of the fold factor goes to its extra slot (the last)
-        const int slot = (lane & tf.x) * tf.y + (cv[f] > 0 ? cv[f] - 1 : tf.y - 1);
+        const int slot = cat_slot(tf, cv[f] > 0 ? cv[f] - 1 : tf.y - 1, lane & tf.x);
         unsigned long long* h = hist + tf.z + slot * a.nd_stride;
         if constexpr (!(DLSA_CAT_ABLATE & 1)) {
           lds_add_u(h, ut[0]);
@@ -304,7 +318,10 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
         const int pn = cat_pair(f, g, FM) + 2;
         const int4 tn = ptab[pn <= kCatMaxPairs ? pn : kCatMaxPairs];
         if (!(DLSA_CAT_ABLATE & 2) && g < F && cv[f] > 0 && cv[g] > 0)
-          lds_add_u(hist + tp.x + ((lane & tp.y) * tp.z + cv[f] - 1) * tp.w + cv[g] - 1, ut[0]);
+          lds_add_u(hist + tp.x +
+                        (DLSA_CAT_RINNER ? ((cv[f] - 1) * tp.w + cv[g] - 1) * (tp.y + 1) + (lane & tp.y)
+                                         : ((lane & tp.y) * tp.z + cv[f] - 1) * tp.w + cv[g] - 1),
+                    ut[0]);
         tp = tp1;
         tp1 = tn;
       }
@@ -362,7 +379,7 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
   auto nd_sum = [&](int f, int lev, int col) {
     const int4 r = ftab[f];  // {R - 1, level slots, nd offset, g offset}
     long long s = 0;
-    for (int rp = 0; rp <= r.x; ++rp) s += hist_at(hist, r.z + (rp * r.y + lev) * a.nd_stride + col);
+    for (int rp = 0; rp <= r.x; ++rp) s += hist_at(hist, r.z + cat_slot(r, lev, rp) * a.nd_stride + col);
     return (double)s / (col == 0 ? hsl[0] : hsl[1 + col]);
   };
   // EX: the intercept row -- the fold factor's bins over every level slot
@@ -373,8 +390,8 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
     long long s = 0;
     for (int rp = 0; rp <= r.x; ++rp)
       for (int l = 0; l < r.y; ++l)
-        s += col < 0 ? hist_at(hist, r.w + rp * r.y + l)
-                     : hist_at(hist, r.z + (rp * r.y + l) * a.nd_stride + col);
+        s += col < 0 ? hist_at(hist, r.w + cat_slot(r, l, rp))
+                     : hist_at(hist, r.z + cat_slot(r, l, rp) * a.nd_stride + col);
     const int si = col < 0 ? 1 : col == 0 ? 0 : 1 + col;  // its grid (hsl layout above)
     return (double)s / hsl[si];
   };
@@ -410,7 +427,9 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
             // {offset, R - 1, L_fj, L_fi} at the pair's row-loop position
             const int4 r = ptab[cat_pair(fj, fi, FM)];
             long long s = 0;
-            for (int rp = 0; rp <= r.y; ++rp) s += hist_at(hist, r.x + (rp * r.z + lj) * r.w + li);
+            for (int rp = 0; rp <= r.y; ++rp)
+              s += hist_at(hist, r.x + (DLSA_CAT_RINNER ? (lj * r.w + li) * (r.y + 1) + rp
+                                                        : (rp * r.z + lj) * r.w + li));
             v = (double)s / hsl[0];
           }
         }
@@ -428,7 +447,7 @@ __global__ __launch_bounds__(NTHR) void cat_pass_kernel(const CatArgs a) {
       const int f = factor_of(e, l);
       const int4 r = ftab[f];
       long long s = 0;
-      for (int rp = 0; rp <= r.x; ++rp) s += hist_at(hist, r.w + rp * r.y + l);
+      for (int rp = 0; rp <= r.x; ++rp) s += hist_at(hist, r.w + cat_slot(r, l, rp));
       v = (double)s / hsl[1];
     }
     a.slab_g[(int64_t)chunk * PP + e] = v;

@@ -286,9 +286,9 @@ struct CatArgs {
                                    // intercept row of X^T W X and gradient are the sums of
                                    // its levels (no register accumulators for them)
   int32_t doff[kCatMaxFactors];    // parameter index of factor f's first dummy
-  int32_t nd_off[kCatMaxFactors];  // LDS: [rep][nlev][q + 1] (w, w x_0 ..)
+  int32_t nd_off[kCatMaxFactors];  // LDS: [rep][level slot][q + 1] (w, w x_0 ..; cat_slot)
   int32_t nd_rep[kCatMaxFactors];  // replicas (power of two)
-  int32_t g_off[kCatMaxFactors];   // LDS: [rep][nlev] gradient
+  int32_t g_off[kCatMaxFactors];   // LDS: [rep][level slot] gradient
   int32_t pr_off[kCatMaxPairs];    // LDS: pair (f < g) [rep][nlev_f][nlev_g]
   int32_t pr_rep[kCatMaxPairs];
   // fixed-point scales of the int64 histograms per partition, device

@@ -22,6 +22,7 @@ for v in "$@"; do
     catnd512) D=DLSA_CAT_ND_CAP=512 ;;
     catpf1) D=DLSA_CAT_PF=1 ;;
     cat32) D="DLSA_CAT_PF=0 -DDLSA_CAT_ABLATE=32" ;;
+    catrin) D=DLSA_CAT_RINNER=1 ;;
     catpf32) D=DLSA_CAT_ABLATE=32 ;;
     solveprof) D=DLSA_SOLVE_PROFILE=1 ;;
     solveblk) D=DLSA_SOLVE_BLOCKED=1 ;;
