@@ -24,6 +24,15 @@
 #ifndef DLSA_OLS_STREAM
 #define DLSA_OLS_STREAM 1
 #endif
+// each k-step group loaded then computed (0), or the next group's loads in
+// flight under the current group's MFMAs in a second register set (1, A/B).
+// Round 6, config 4, alternated: two sets measured 12.08-12.44 ms per pass at
+// KS = 2 / 3 / 4 and 12.7 at 6, one set (KS = 8) 12.06-12.11
+// (profiles/r06q_ols_prefetch_ab.txt): with 2-3 waves per SIMD the loads of
+// one wave already run under the other waves' MFMAs
+#ifndef DLSA_OLS_PF
+#define DLSA_OLS_PF 0
+#endif
 
 namespace dlsa {
 
@@ -101,8 +110,7 @@ __global__ __launch_bounds__(64 * kOlsWaves) void ols_stream_kernel(const PassAr
   // overlaps them: FULL groups (every lane's feature a column of X) feed the
   // loaded values to the MFMAs as they are; otherwise one select per value
   // (padding features, the intercept column, rows past the chunk).
-  for (int r0 = 0; r0 < nrows; r0 += 4 * KS) {
-    double xv[KS][NT], yv[KS];
+  auto load_group = [&](int r0, double (&xv)[KS][NT], double (&yv)[KS]) {
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const int so = __builtin_amdgcn_readfirstlane((r0 + 4 * s) * p * 8);
@@ -112,6 +120,8 @@ __global__ __launch_bounds__(64 * kOlsWaves) void ols_stream_kernel(const PassAr
       yv[s] = __builtin_bit_cast(
           double, __builtin_amdgcn_raw_buffer_load_b64(yr, q * 8, __builtin_amdgcn_readfirstlane((r0 + 4 * s) * 8), 0));
     }
+  };
+  auto compute_group = [&](int r0, const double (&xv)[KS][NT], const double (&yv)[KS]) {
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       // (a row past the chunk loads 0, which standardisation would shift)
@@ -139,7 +149,30 @@ __global__ __launch_bounds__(64 * kOlsWaves) void ols_stream_kernel(const PassAr
           acc[I * (I + 1) / 2 + J] = __builtin_amdgcn_mfma_f64_16x16x4f64(
               v[I], v[J], acc[I * (I + 1) / 2 + J], 0, 0, 0);
     }
+  };
+  constexpr int GR = 4 * KS;  // rows per group
+#if DLSA_OLS_PF
+  // two register sets: the next group's loads are in flight while the
+  // current group's MFMAs run (the loop is unrolled by two, so no register
+  // copies cross the back edge; no early exit, which made the compiler keep a
+  // second set of accumulators).  A group past the chunk loads 0 from the
+  // bounds-checked buffers and adds zeros (masked when not FULL), in the
+  // single-set loop's accumulation order
+  double xa[KS][NT], ya[KS], xb[KS][NT], yb[KS];
+  load_group(0, xa, ya);
+  for (int r0 = 0; r0 < nrows; r0 += 2 * GR) {
+    load_group(r0 + GR, xb, yb);
+    compute_group(r0, xa, ya);
+    load_group(r0 + 2 * GR, xa, ya);
+    compute_group(r0 + GR, xb, yb);
   }
+#else
+  for (int r0 = 0; r0 < nrows; r0 += GR) {
+    double xv[KS][NT], yv[KS];
+    load_group(r0, xv, yv);
+    compute_group(r0, xv, yv);
+  }
+#endif
 
   // ---- epilogue: the chunk's slab (f64 16x16x4 C/D map: row q + 4 r, column fl)
   double* sH = a.slab_H + (int64_t)chunk * T * 256;

@@ -60,6 +60,9 @@ for v in "$@"; do
     olsks2) D=DLSA_OLS_KS=2 ;;
     olsks2k) D="DLSA_OLS_KS=2 -DDLSA_ENV_KNOBS=1" ;;
     olsks8) D=DLSA_OLS_KS=8 ;;
+    olspf4) D="DLSA_OLS_KS=4 -DDLSA_OLS_PF=1" ;;
+    olspf3) D="DLSA_OLS_KS=3 -DDLSA_OLS_PF=1" ;;
+    olspf2) D="DLSA_OLS_KS=2 -DDLSA_OLS_PF=1" ;;
     olsks12) D=DLSA_OLS_KS=12 ;;
     olsks16) D=DLSA_OLS_KS=16 ;;
     wnprof) D=DLSA_WN_PROF=1 ;;
@@ -76,7 +79,7 @@ for v in "$@"; do
     solve*) ONLY='["newton_solve.hip"]' ;;
     catnd*) ONLY='["capi.hip"]' ;;
     cat*) ONLY='["cat_pass.hip"]' ;;
-    olswave|olsks2|olsks8|olsks12|olsks16) ONLY='["ols_stream.hip"]' ;;
+    olswave|olspf4|olspf3|olspf2|olsks2|olsks8|olsks12|olsks16) ONLY='["ols_stream.hip"]' ;;
     olsks2k) ONLY='["ols_stream.hip", "capi.hip"]' ;;
     wn*|wrow*) ONLY='["wide_pass.hip"]' ;;
     knobs) ONLY='["capi.hip"]' ;;
