@@ -122,19 +122,22 @@ hipError_t launch_fit_finalize(int K, int P, const double* theta, const double* 
 
 // theta_rec[k] = theta[k] for the partitions whose phase is ph: the point at
 // which the next bf16 pass records their Ozaki digit scales
+// gate: null, or the snapshot is taken only if gate[0] > 0 (the pass it
+// belongs to records max |z| under the same condition, PassArgs::zrec_gate)
 __global__ void theta_snapshot_kernel(int K, int P, const int32_t* phase, int ph,
-                                      const double* theta, double* theta_rec) {
+                                      const double* theta, double* theta_rec, const int32_t* gate) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (int64_t)K * P) return;
+  if (gate && gate[0] <= 0) return;
   if (phase[i / P] == ph) theta_rec[i] = theta[i];
 }
 
 hipError_t launch_theta_snapshot(int K, int P, const int32_t* phase, int ph, const double* theta,
-                                 double* theta_rec, hipStream_t s) {
+                                 double* theta_rec, hipStream_t s, const int32_t* gate) {
   const int64_t n = (int64_t)K * P;
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(theta_snapshot_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, K,
-                     P, phase, ph, theta, theta_rec);
+                     P, phase, ph, theta, theta_rec, gate);
   return hipGetLastError();
 }
 

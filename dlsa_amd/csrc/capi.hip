@@ -91,6 +91,11 @@ static int64_t rows_used(int64_t nk, double frac, int64_t min_rows) {
   if (frac >= 1.0) return nk;
   return std::min(nk, std::max(min_rows, (int64_t)std::ceil(frac * (double)nk)));
 }
+// the next iteration's approximate pass enqueued before the host reads the
+// counters (1) or after (0, A/B; fit_impl's spec_pass)
+#ifndef DLSA_SPEC_PASS
+#define DLSA_SPEC_PASS 1
+#endif
 // warm-start row-prefix fractions (ascending, each < 1); DLSA_LEVELS="a,b,..."
 // overrides (schedule sweeps, tools/level_sweep.sh), DLSA_LEVELS="" disables.
 // A level using more than half of all rows is skipped, so "x,0.5" runs as
@@ -1197,11 +1202,46 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
     }
     return e;
   };
+  // The next iteration's approximate pass is enqueued before the host reads
+  // this iteration's counters (DLSA_SPEC_PASS): a pass checks its partitions'
+  // phases on the device, so one enqueued for partitions that have since
+  // switched or finished runs as a no-op, and the GPU no longer idles through
+  // every hand-back (hipStreamSynchronize's return, the host's decisions and
+  // the next launch: 25-45 us per iteration).  The one decision
+  // such a pass needs from those counters -- whether to record max |z| (a
+  // partition near the switch, counters[3]) -- is taken on the device
+  // (PassArgs::zrec_gate, the gated theta snapshot), and the host's
+  // bookkeeping of the pass (zfresh, stats) runs after the read, from the
+  // phases the pass saw.
+  struct ReadEvent {  // the counters' copy of an iteration (destroyed on every return)
+    hipEvent_t ev = nullptr;
+    ~ReadEvent() {
+      if (ev) (void)hipEventDestroy(ev);
+    }
+  } read_ev;
+  if (DLSA_SPEC_PASS) DLSA_HIP_TRY(hipEventCreateWithFlags(&read_ev.ev, hipEventDisableTiming));
+  auto spec_pass = [&](const Plan& q, bool full) -> hipError_t {
+    pa.want_phase = PHASE_F32;
+    const bool zg = use_oz && full && zrec;
+    if (zg) {
+      hipError_t e = launch_theta_snapshot(K, P, d_phase, PHASE_F32, theta, d_threc, stream, d_cnt + 3);
+      if (e != hipSuccess) return e;
+    }
+    return timed(&g_stats.ms_pass_fp32, [&] {
+      PassArgs pc = pa;
+      pc.colmax = nullptr;
+      pc.zcolmax = zg ? d_zcolmax : nullptr;
+      pc.theta_rec = d_threc;
+      pc.zrec_gate = zg ? d_cnt + 3 : nullptr;
+      return launch_irls_coop(pc, q.NT, approx_prec, standardize, family, q.n_chunks, stream);
+    });
+  };
   int it = 0;
   for (size_t lvl = 0; lvl < plans.size(); ++lvl) {
     const Plan& q = plans[lvl];
     const bool final_level = lvl + 1 == plans.size();
     const std::vector<int64_t> part_rows = plan_part_rows(q, K);
+    bool spec = false;  // this iteration's PHASE_F32 pass was enqueued before the last read
     DLSA_HIP_TRY(upload(q));
     if (lvl > 0) {  // re-enter every running partition
       DLSA_HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, stream));
@@ -1227,6 +1267,17 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
     for (; it < it_end && running_total(n_running) > 0 && q.n_chunks > 0; ++it) {
       // approximate (bf16 or fp32), escalated fp32, then exact passes
       for (int ph : {PHASE_F32, PHASE_F32X, PHASE_F64}) {
+        if (ph == PHASE_F32 && spec) {
+          // enqueued before the last read: its bookkeeping, from the phases it saw
+          if (n_running[ph] > 0) {
+            const bool rz = use_oz && final_level && zrec && near_switch;  // the device's decision
+            for (int k = 0; k < K; ++k)
+              if (h_phase[k] == ph) zfresh[k] = rz;
+            g_stats.passes_fp32++;
+            g_stats.rows_fp32 += phase_rows(part_rows, h_phase, ph);
+          }
+          continue;
+        }
         if (n_running[ph] == 0) continue;
         DLSA_HIP_TRY(fused_pass(ph, q, final_level, part_rows, h_phase));
       }
@@ -1234,7 +1285,18 @@ static int fit_impl(int family, const double* X, const double* y, const int64_t*
       DLSA_HIP_TRY(timed(&g_stats.ms_solve, [&] { return launch_newton_solve(sa, K, stream); }));
       // counters + phases in one copy (adjacent on both sides)
       DLSA_HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 16 + 4LL * K, hipMemcpyDeviceToHost, stream));
-      DLSA_HIP_TRY(hipStreamSynchronize(stream));
+      // the next iteration's approximate pass, if this one had approximate
+      // partitions and the next needs no first max |x| record (rec_x)
+      spec = DLSA_SPEC_PASS && n_running[PHASE_F32] > 0 && it + 1 < it_end &&
+             !(use_oz && final_level && !colmax_ready);
+      if (spec) {
+        // wait for the copy only: the pass runs on while the host decides
+        DLSA_HIP_TRY(hipEventRecord(read_ev.ev, stream));
+        DLSA_HIP_TRY(spec_pass(q, final_level));
+        DLSA_HIP_TRY(hipEventSynchronize(read_ev.ev));
+      } else {
+        DLSA_HIP_TRY(hipStreamSynchronize(stream));
+      }
       for (int ph = 0; ph < kRunPhases; ++ph) n_running[ph] = h_cnt[ph];
       near_switch = final_level && h_cnt[3] > 0;
       if (trace) DLSA_HIP_TRY(trace_iteration(K, P, theta, d_dprev, lvl, it, n_running));

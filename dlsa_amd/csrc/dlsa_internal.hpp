@@ -84,6 +84,9 @@ struct PassArgs {
   uint32_t* colmax;
   uint32_t* zcolmax;
   const double* theta_rec;
+  // null, or zcolmax is written only if zrec_gate[0] > 0: the near-switch
+  // count of the solve before, for a pass enqueued before the host read it
+  const int32_t* zrec_gate;
   int32_t waves;  // fp64 per-wave pass geometry (dlsa_fit_options.exact_waves; 0 = auto)
 };
 
@@ -369,7 +372,7 @@ hipError_t launch_polish_mark(int K, int32_t* phase, const int32_t* status, int3
 // theta_rec[k] = theta[k] for the partitions in phase `ph` (before a pass
 // that records the Ozaki digit scales)
 hipError_t launch_theta_snapshot(int K, int P, const int32_t* phase, int ph, const double* theta,
-                                 double* theta_rec, hipStream_t s);
+                                 double* theta_rec, hipStream_t s, const int32_t* gate = nullptr);
 hipError_t launch_fit_finalize(int K, int P, const double* theta, const double* sig_inv,
                                double* sig_inv_theta, int32_t* status, hipStream_t s);
 hipError_t launch_reduce_partitions(const double* sig_inv, const double* sig_inv_theta,

@@ -560,6 +560,9 @@ void irls_coop_kernel(const PassArgs a) {
       }
     }
     __syncthreads();
+    // a pass enqueued before the host read the near-switch count records only
+    // if that count is > 0 (the running max costs one fp32 max per value)
+    const bool zon = (CM & 2) && (a.zrec_gate == nullptr || a.zrec_gate[0] > 0);
     for (int f = tid; f < G::PMAX; f += 64 * W) {
       uint32_t v = 0, u = 0;
 #pragma unroll
@@ -568,7 +571,8 @@ void irls_coop_kernel(const PassArgs a) {
         u = max(u, cred[(W + w) * G::PMAX + f]);
       }
       if constexpr (CM & 1) a.colmax[(int64_t)chunk * G::PMAX + f] = v;
-      if constexpr (CM & 2) a.zcolmax[(int64_t)chunk * G::PMAX + f] = u;
+      if constexpr (CM & 2)
+        if (zon) a.zcolmax[(int64_t)chunk * G::PMAX + f] = u;
     }
   }
 }

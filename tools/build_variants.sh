@@ -48,6 +48,7 @@ for v in "$@"; do
     ozovl) D="DLSA_OZ_OVL=1" ;;
     ozquad) D="DLSA_OZ_R4=0 -DDLSA_OZ_EDGE=0" ;;
     knobs) D=DLSA_ENV_KNOBS=1 ;;
+    nospec) D=DLSA_SPEC_PASS=0 ;;
     ozs1) D=DLSA_OZ_SCHED=1 ;;
     ozs2) D=DLSA_OZ_SCHED=2 ;;
     oz6) D=DLSA_OZ_LEVELS=6 ;;
@@ -82,7 +83,7 @@ for v in "$@"; do
     olswave|olspf4|olspf3|olspf2|olsks2|olsks8|olsks12|olsks16) ONLY='["ols_stream.hip"]' ;;
     olsks2k) ONLY='["ols_stream.hip", "capi.hip"]' ;;
     wn*|wrow*) ONLY='["wide_pass.hip"]' ;;
-    knobs) ONLY='["capi.hip"]' ;;
+    knobs|nospec) ONLY='["capi.hip"]' ;;
     cmabl) ONLY='["irls_coop_g1.hip", "irls_coop_g2.hip", "irls_coop_g3.hip", "irls_coop_g4.hip", "irls_coop_g5.hip", "irls_coop_g6.hip"]' ;;
     ols*|wslot3) ONLY='["irls_wave.hip", "irls_wave_g2.hip"]' ;;
   esac
